@@ -1,0 +1,227 @@
+#!/usr/bin/env python3
+"""Benchmark: Msamples/s + achieved bytes/s of the render kernel on the RTOW final scene.
+
+One step = one whole frame of BASELINE config 2 (rtweekend_final_image scene at set_seed(42),
+1200x800, 500 spp, max_depth 50) rendered by the gfx950 kernel from a scene already resident in
+HBM. With N ranks (torchrun, one process per GPU) the frame's rows are dealt to ranks in 16-row
+blocks, each rank renders its blocks, and the tiles are all-gathered over RCCL (xGMI) into a full
+frame on every rank: the total work is fixed, so scaling is "strong".
+
+Prints ONE JSON line on rank 0 (see the repo contract), with
+  roofline:     algorithmic bytes of the render kernel (56 B per BVH node visited,
+                36 B per sphere test, 124 B per parallelogram test, 24 B per pixel written; the
+                visit counts come from an untimed instrumented pass of the same frame) / the
+                kernel's average launch time (HIP events on the launch stream), against the HBM
+                peak 8 TB/s; traffic from profiles/ PMC data when present.
+  cpu_baseline: the reference's own Camera::render (oracle/_ref, built from the reference
+                sources) timed on this host's cores over a bounded sample of the same scene.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
+FP64_VECTOR_PEAK_TFLOPS = 78.6  # MI355X spec (vector FP64)
+NODE_B, SPHERE_B, QUAD_B, PIXEL_B = 56, 36, 124, 24
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--scene", default="rtow_final")
+    ap.add_argument("--seed", type=int, default=42)
+    ap.add_argument("--width", type=int, default=1200)
+    ap.add_argument("--height", type=int, default=800)
+    ap.add_argument("--spp", type=int, default=500)
+    ap.add_argument("--depth", type=int, default=50)
+    ap.add_argument("--base-seed", type=int, default=2024)
+    ap.add_argument("--cpu-spp", type=int, default=40, help="spp of the bounded CPU-baseline sample")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, host cores)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--pmc-json", default=str(ROOT / "profiles" / "pmc_latest.json"))
+    return ap.parse_args()
+
+
+def cpu_baseline(args, scene_data, log) -> dict | None:
+    """Reference Camera::render on the host, on a bounded sample of the same workload."""
+    import cpp_raytracer_amd as crt
+    from cpp_raytracer_amd import camera_with
+    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+    ref = ROOT / "oracle" / "_ref" / "ref_driver"
+    sample = f"{args.scene} seed {args.seed}, {args.width}x{args.height}, {args.cpu_spp} spp, depth {args.depth}"
+    d = crt.SceneData(scene_data.materials, scene_data.objects,
+                      camera_with(scene_data.camera, image_w=args.width, image_h=args.height,
+                                  samples_per_pixel=args.cpu_spp, max_depth=args.depth))
+    with tempfile.TemporaryDirectory() as td:
+        p = Path(td) / "scene.crts"
+        d.save(p)
+        if ref.exists():
+            try:
+                r = subprocess.run([str(ref), "time", str(p), str(threads)], capture_output=True, text=True,
+                                   timeout=600, check=True)
+                j = json.loads(r.stdout.strip().splitlines()[-1])
+                return {"value": round(j["samples"] / j["seconds"] / 1e6, 4), "unit": "Msamples/s",
+                        "cores": threads, "kind": "reference",
+                        "sample": sample + " (reference Camera::render, OpenMP, own per-thread RNG)"}
+            except Exception as e:  # pragma: no cover - reported, not fatal
+                log(f"reference CPU baseline failed: {e}")
+        try:
+            sys.path.insert(0, str(ROOT / "oracle"))
+            import crt_oracle_py as orc
+            secs, n = orc.time_render(d, threads, args.base_seed)
+            return {"value": round(n / secs / 1e6, 4), "unit": "Msamples/s", "cores": threads, "kind": "port",
+                    "sample": sample + " (oracle C restatement, OpenMP)"}
+        except Exception as e:  # pragma: no cover
+            log(f"port CPU baseline failed: {e}")
+    return None
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    import cpp_raytracer_amd as crt
+    from cpp_raytracer_amd import Tiling, camera_with
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        args.gpus = world if world > 1 else args.gpus
+    distributed = world > 1
+    torch.cuda.set_device(local)
+    if distributed:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    def log(msg):
+        if rank == 0:
+            print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+    t0 = time.time()
+    data = crt.SceneData.named(args.scene, args.seed)
+    data.camera = camera_with(data.camera, image_w=args.width, image_h=args.height,
+                              samples_per_pixel=args.spp, max_depth=args.depth)
+    scene = crt.GpuScene(data)
+    info = scene.info()
+    scene.upload(local)
+    cam = crt.resolve_camera(data.camera, args.base_seed)
+    h, w = args.height, args.width
+    rb = 16
+    tiling = Tiling(rb, world, rank, 0)
+    owned = [r for r in range(h) if (r // rb) % world == rank]
+    max_owned = max(sum(1 for r in range(h) if (r // rb) % world == k) for k in range(world))
+    log(f"scene {args.scene}: {info.num_primitives} prims, {info.num_nodes} nodes, depth {info.depth}, "
+        f"BVH build {info.build_ms:.1f} ms, setup {time.time() - t0:.1f} s")
+
+    frame = torch.zeros(h, w, 3, dtype=torch.float64, device="cuda")
+    owned_idx = torch.tensor(owned, dtype=torch.long, device="cuda")
+    tile = torch.zeros(max_owned, w, 3, dtype=torch.float64, device="cuda")
+    gathered = torch.zeros(world * max_owned, w, 3, dtype=torch.float64, device="cuda") if distributed else None
+    stream = torch.cuda.current_stream()
+
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record(stream)
+        scene.render_async(local, cam, frame.data_ptr(), stream.cuda_stream, tiling)
+        if ev is not None:
+            ev[1].record(stream)
+        if distributed:  # gather the row tiles (RCCL all-gather over xGMI)
+            tile[: len(owned)].copy_(frame.index_select(0, owned_idx))
+            dist.all_gather_into_tensor(gathered, tile)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t_start = time.perf_counter()
+    for i in range(args.steps):
+        step(evs[i])
+    torch.cuda.synchronize()
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t_start
+    kernel_ms = sum(a.elapsed_time(b) for a, b in evs) / max(1, args.steps)
+    if distributed:
+        t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kernel_ms = float(t[0]), float(t[1])
+    samples_total = h * w * args.spp * args.steps
+    ms_per_step = elapsed * 1e3 / max(1, args.steps)
+
+    # algorithmic bytes of one launch (this rank's tile), from the instrumented pass (untimed)
+    cnt = scene.render_count(local, cam, tiling)
+    alg_bytes = (cnt.nodes_visited * NODE_B + cnt.sphere_tests * SPHERE_B + cnt.parallelogram_tests * QUAD_B
+                 + len(owned) * w * PIXEL_B)
+    rays_per_sample = cnt.rays / max(1, cnt.samples)
+    flops = cnt.nodes_visited * 12 + cnt.sphere_tests * 23 + cnt.parallelogram_tests * 40 + cnt.rays * 50
+    achieved_gbs = alg_bytes / (kernel_ms * 1e-3) / 1e9
+    traffic = None
+    pmc = Path(args.pmc_json)
+    if pmc.exists():
+        try:
+            pj = json.loads(pmc.read_text())
+            if pj.get("workload") == f"{args.scene}:{w}x{h}x{args.spp}:d{args.depth}:n{world}":
+                traffic = pj.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    if distributed:
+        t = torch.tensor([alg_bytes, cnt.rays, cnt.samples, cnt.nodes_visited], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t)  # totals for the record
+    if rank == 0:
+        cpu = None if args.no_cpu_baseline else cpu_baseline(args, data, log)
+        out = {
+            "metric": "Msamples/sec + achieved HBM GB/s, RTOW final scene at 1/2/4/8 MI355X",
+            "value": round(samples_total / elapsed / 1e6, 3),
+            "unit": "Msamples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic: rtweekend_final_image scene built by the reference's RNG at set_seed(42)",
+            "config": {"workload": f"{args.scene} seed {args.seed}, {w}x{h}, {args.spp} spp, max_depth {args.depth}"
+                                   f" (BASELINE config 2)" if (args.scene, w, h, args.spp, args.depth) ==
+                                   ("rtow_final", 1200, 800, 500, 50) else
+                                   f"{args.scene} seed {args.seed}, {w}x{h}, {args.spp} spp, max_depth {args.depth}",
+                       "samples_per_step": h * w * args.spp, "primitives": int(info.num_primitives),
+                       "bvh_nodes": int(info.num_nodes), "partition": f"16-row blocks over {world} ranks, "
+                       "RCCL all-gather of tiles" if distributed else "whole frame on one GPU"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved_gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "kernel_ms": round(kernel_ms, 3),
+                         "alg_bytes_per_launch": int(alg_bytes),
+                         "basis": "SURVEY 8d algorithmic bytes (56 B/node, 36 B/sphere test, 124 B/quad test, "
+                                  "24 B/pixel); scene is LDS/L1/L2-resident, so these bytes mostly never reach HBM"},
+            "fp64": {"achieved_tflops": round(flops / (kernel_ms * 1e-3) / 1e12, 3),
+                     "peak_tflops": FP64_VECTOR_PEAK_TFLOPS, "rays_per_sample": round(rays_per_sample, 4),
+                     "nodes_per_ray": round(cnt.nodes_visited / max(1, cnt.rays), 3),
+                     "prim_tests_per_ray": round((cnt.sphere_tests + cnt.parallelogram_tests) / max(1, cnt.rays), 3)},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if distributed:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,147 @@
+"""ctypes binding of the C ABI in include/crt_render.h (libcrt_hip.so, built in-tree).
+
+The library is the product: there is no Python or CPU fallback for the render path. Loading
+fails loudly if the in-tree .so is missing; rendering fails loudly if no GPU is visible.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+import numpy as np
+
+PKG_DIR = Path(__file__).resolve().parent
+LIB_PATH = PKG_DIR / "lib" / "libcrt_hip.so"
+
+CRT_LAMBERTIAN, CRT_METAL, CRT_DIELECTRIC, CRT_DIFFUSE_LIGHT = 1, 2, 3, 4
+CRT_SPHERE, CRT_PARALLELOGRAM, CRT_BOX = 1, 2, 3
+
+D3 = C.c_double * 3
+
+
+class Material(C.Structure):
+    _fields_ = [("kind", C.c_uint32), ("reserved", C.c_uint32), ("color", D3), ("param", C.c_double)]
+
+
+class Object(C.Structure):
+    _fields_ = [("kind", C.c_uint32), ("material", C.c_uint32), ("v", C.c_double * 9)]
+
+
+class BVHParams(C.Structure):
+    _fields_ = [("num_buckets", C.c_uint32), ("max_prims_in_node", C.c_uint32),
+                ("linear", C.c_uint32), ("reserved", C.c_uint32)]
+
+
+class CameraSettings(C.Structure):
+    _fields_ = [("image_w", C.c_uint32), ("image_h", C.c_uint32),
+                ("samples_per_pixel", C.c_uint32), ("max_depth", C.c_uint32),
+                ("center", D3), ("direction", D3), ("lookat", D3), ("up", D3),
+                ("focus_dist", C.c_double), ("fov", C.c_double), ("defocus_angle", C.c_double),
+                ("background", D3),
+                ("has_lookat", C.c_uint32), ("has_focus_dist", C.c_uint32),
+                ("fov_is_vertical", C.c_uint32), ("reserved", C.c_uint32)]
+
+
+class Camera(C.Structure):
+    _fields_ = [("image_w", C.c_uint32), ("image_h", C.c_uint32),
+                ("samples_per_pixel", C.c_uint32), ("max_depth", C.c_uint32),
+                ("origin", D3), ("pixel00", D3), ("pixel_delta_x", D3), ("pixel_delta_y", D3),
+                ("defocus_disk_x", D3), ("defocus_disk_y", D3),
+                ("defocus_angle", C.c_double), ("background", D3), ("t_min", C.c_double),
+                ("base_seed", C.c_uint32), ("reserved", C.c_uint32)]
+
+
+class Tiling(C.Structure):
+    _fields_ = [("row_block", C.c_uint32), ("tile_count", C.c_uint32),
+                ("tile_index", C.c_uint32), ("reserved", C.c_uint32)]
+
+
+class SceneInfo(C.Structure):
+    _fields_ = [("num_objects", C.c_uint64), ("num_materials", C.c_uint64),
+                ("num_primitives", C.c_uint64), ("num_spheres", C.c_uint64),
+                ("num_parallelograms", C.c_uint64), ("num_nodes", C.c_uint64),
+                ("depth", C.c_uint32), ("max_leaf_size", C.c_uint32),
+                ("device_bytes", C.c_uint64), ("build_ms", C.c_double)]
+
+
+class BVHNode(C.Structure):
+    _fields_ = [("bounds", C.c_double * 6), ("index", C.c_uint32), ("count", C.c_uint32),
+                ("axis", C.c_uint32), ("flags", C.c_uint32)]
+
+
+class Hit(C.Structure):
+    _fields_ = [("t", C.c_double), ("point", D3), ("normal", D3), ("prim", C.c_int32),
+                ("front_face", C.c_int32), ("material", C.c_uint32), ("reserved", C.c_uint32)]
+
+
+class RenderStats(C.Structure):
+    _fields_ = [("samples", C.c_uint64), ("rays", C.c_uint64), ("nodes_visited", C.c_uint64),
+                ("sphere_tests", C.c_uint64), ("parallelogram_tests", C.c_uint64),
+                ("kernel_ms", C.c_double)]
+
+
+# numpy views of the same records (for bulk scene I/O)
+MATERIAL_DTYPE = np.dtype([("kind", "<u4"), ("reserved", "<u4"), ("color", "<f8", 3), ("param", "<f8")])
+OBJECT_DTYPE = np.dtype([("kind", "<u4"), ("material", "<u4"), ("v", "<f8", 9)])
+NODE_DTYPE = np.dtype([("bounds", "<f8", 6), ("index", "<u4"), ("count", "<u4"), ("axis", "<u4"),
+                       ("flags", "<u4")])
+HIT_DTYPE = np.dtype([("t", "<f8"), ("point", "<f8", 3), ("normal", "<f8", 3), ("prim", "<i4"),
+                      ("front_face", "<i4"), ("material", "<u4"), ("reserved", "<u4")])
+assert MATERIAL_DTYPE.itemsize == C.sizeof(Material) == 40
+assert OBJECT_DTYPE.itemsize == C.sizeof(Object) == 80
+assert NODE_DTYPE.itemsize == C.sizeof(BVHNode) == 64
+assert HIT_DTYPE.itemsize == C.sizeof(Hit)
+
+P = C.POINTER
+EXPORTS = {
+    "crt_abi_version": (C.c_int, []),
+    "crt_last_error": (C.c_char_p, []),
+    "crt_device_count": (C.c_int, [P(C.c_int)]),
+    "crt_free": (None, [C.c_void_p]),
+    "crt_sample_seed": (C.c_uint32, [C.c_uint32, C.c_uint32, C.c_uint32]),
+    "crt_rand_double": (C.c_double, [P(C.c_uint32), C.c_double, C.c_double]),
+    "crt_scene_build_named": (C.c_int, [C.c_char_p, C.c_uint32, C.c_int, P(P(Material)), P(C.c_size_t),
+                                        P(P(Object)), P(C.c_size_t), P(CameraSettings)]),
+    "crt_scene_create": (C.c_int, [C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t, P(BVHParams),
+                                   P(C.c_void_p)]),
+    "crt_scene_info_get": (C.c_int, [C.c_void_p, P(SceneInfo)]),
+    "crt_scene_export_bvh": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
+    "crt_scene_upload": (C.c_int, [C.c_void_p, C.c_int]),
+    "crt_scene_destroy": (None, [C.c_void_p]),
+    "crt_camera_resolve": (C.c_int, [P(CameraSettings), P(Camera)]),
+    "crt_render_async": (C.c_int, [C.c_void_p, C.c_int, P(Camera), P(Tiling), C.c_void_p, C.c_void_p]),
+    "crt_render_count": (C.c_int, [C.c_void_p, C.c_int, P(Camera), P(Tiling), P(RenderStats)]),
+    "crt_render": (C.c_int, [C.c_void_p, P(Camera), C.c_int, C.c_void_p, P(RenderStats)]),
+    "crt_closest_hits": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t, C.c_double, C.c_double,
+                                   C.c_void_p]),
+}
+
+
+class CrtError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    """Load the in-tree library (once). Raises if it has not been built."""
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            raise CrtError(f"{LIB_PATH} is missing: run __graft_entry__.build() "
+                           "(make -C cpp_raytracer_amd); there is no fallback path")
+        h = C.CDLL(str(LIB_PATH), mode=os.RTLD_NOW | C.RTLD_GLOBAL)
+        for name, (res, args) in EXPORTS.items():
+            f = getattr(h, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = h
+    return _lib
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != 0:
+        msg = lib().crt_last_error().decode(errors="replace")
+        raise CrtError(f"{what or 'crt'} failed ({rc}): {msg}")

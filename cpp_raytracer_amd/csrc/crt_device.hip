@@ -1,0 +1,869 @@
+// gfx950 render path: the reference's per-pixel/per-sample loop (camera.h:264-297), recursive
+// integrator (camera.h:205-258), BVH traversal (bvh.h:585-715), primitive tests (sphere.h:45-96,
+// parallelogram.h:177-240) and material scatter (material.h:64-263) as ONE kernel.
+//
+// Numerics: IEEE double throughout, compiled with -ffp-contract=off, every expression in the
+// reference's operation order, so the geometry of each path (hit points, directions, RNG
+// decisions) is bit-identical to the reference's for the same per-sample RNG stream. Radiance is
+// accumulated forward (throughput) instead of by recursion; that re-association moves a
+// sample's colour by a few ulps and never changes a path.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <limits>
+#include <string>
+#include <vector>
+
+#include "crt_internal.h"
+
+#pragma clang fp contract(off)
+
+namespace crt {
+
+#define HIP_TRY(expr)                                                                     \
+    do {                                                                                  \
+        hipError_t e_ = (expr);                                                           \
+        if (e_ != hipSuccess)                                                             \
+            return fail(CRT_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));    \
+    } while (0)
+
+namespace dev {
+
+constexpr int kBlock = 256;          // 4 waves; each wave owns one 8x8 pixel tile
+constexpr double kScale = 1 / static_cast<double>(4294967295u - 1);  // rand_util.h:110-112
+
+struct SceneView {
+    const DevNode* nodes;
+    const uint32_t* refs;
+    const DevSphere* spheres;
+    const uint32_t* sphere_mat;
+    const DevQuad* quads;
+    const uint32_t* quad_mat;
+    const DevMaterial* mats;
+};
+
+struct CamView {
+    double o[3], p00[3], pdx[3], pdy[3], ddx[3], ddy[3];
+    double defocus_angle;
+    double bg[3];
+    double t_min;
+    double inv_spp;
+    uint32_t w, h, spp, max_depth, base_seed;
+};
+
+struct Work {
+    uint32_t owned_rows;   // rows of this tiling
+    uint32_t row_block, tile_count, tile_index;
+    uint32_t tiles_x, tiles_y, tiles;  // 8x8 pixel tiles over (owned rows x width)
+    uint32_t chunks, chunk_len;        // sample chunks per pixel
+};
+
+struct Counters {
+    unsigned long long rays, nodes, sphere_tests, quad_tests;
+};
+
+// ---- reference RNG (rand_util.h:85-117) with per-sample state ------------------------------
+__device__ __forceinline__ double rnd(uint32_t& s, double lo, double hi) {
+    s = 1664525u * s + 1013904223u;
+    return lo + (hi - lo) * static_cast<double>(s) * kScale;
+}
+
+__device__ __forceinline__ uint32_t sample_seed(uint32_t base, uint32_t pixel, uint32_t sample) {
+    uint64_t z = (static_cast<uint64_t>(pixel) << 32) | sample;
+    z += static_cast<uint64_t>(base) * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    return static_cast<uint32_t>(z ^ (z >> 32));
+}
+
+// Vec3D::random_unit_vector (vec3d.h:64-75): rejection in the cube, then * (1 / |v|)
+__device__ __forceinline__ void random_unit_vector(uint32_t& s, double& x, double& y, double& z) {
+    double m2;
+    do {
+        x = rnd(s, -1, 1);
+        y = rnd(s, -1, 1);
+        z = rnd(s, -1, 1);
+        m2 = x * x + y * y + z * z;
+    } while (!(m2 < 1));
+    double inv = 1 / sqrt(x * x + y * y + z * z);
+    x = x * inv;
+    y = y * inv;
+    z = z * inv;
+}
+
+// x^5 rounded once from a double-double product (std::pow(1 - cos, 5), material.h:180)
+__device__ __forceinline__ double pow5(double x) {
+    double x2h = x * x;
+    double x2l = __builtin_fma(x, x, -x2h);
+    double x4h = x2h * x2h;
+    double x4l = __builtin_fma(x2h, x2h, -x4h) + 2 * x2h * x2l;
+    double x5h = x4h * x;
+    double x5l = __builtin_fma(x4h, x, -x5h) + x4l * x;
+    return x5h + x5l;
+}
+
+// AABB::is_hit_by_optimized (aabb.h:132-174)
+__device__ __forceinline__ bool slab(const DevNode& n, const double o[3], const double inv[3],
+                                     const int neg[3], double tmin, double tmax) {
+    double xtmin = (n.b[0 + neg[0]] - o[0]) * inv[0];
+    double xtmax = (n.b[1 - neg[0]] - o[0]) * inv[0];
+    double ytmin = (n.b[2 + neg[1]] - o[1]) * inv[1];
+    double ytmax = (n.b[3 - neg[1]] - o[1]) * inv[1];
+    if (xtmin > ytmax || ytmin > xtmax) return false;
+    if (ytmin > xtmin) xtmin = ytmin;
+    if (ytmax < xtmax) xtmax = ytmax;
+    double ztmin = (n.b[4 + neg[2]] - o[2]) * inv[2];
+    double ztmax = (n.b[5 - neg[2]] - o[2]) * inv[2];
+    if (xtmin > ztmax || ztmin > xtmax) return false;
+    if (ztmin > xtmin) xtmin = ztmin;
+    if (ztmax < xtmax) xtmax = ztmax;
+    return (xtmin < tmax) && (xtmax > tmin);
+}
+
+// Sphere::hit_by (sphere.h:45-96) returning the accepted root through t
+__device__ __forceinline__ bool hit_sphere(const DevSphere& sp, const double o[3], const double d[3],
+                                           double a, double tmin, double tmax, double& t) {
+    double ocx = o[0] - sp.c[0], ocy = o[1] - sp.c[1], ocz = o[2] - sp.c[2];
+    double b = d[0] * ocx + d[1] * ocy + d[2] * ocz;
+    double c = (ocx * ocx + ocy * ocy + ocz * ocz) - sp.r * sp.r;
+    double disc = b * b - a * c;
+    if (disc < 0) return false;
+    double sq = sqrt(disc);
+    double root = (-b - sq) / a;
+    if (!(tmin < root && root < tmax)) {
+        root = (-b + sq) / a;
+        if (!(tmin < root && root < tmax)) return false;
+    }
+    t = root;
+    return true;
+}
+
+// Parallelogram::hit_by (parallelogram.h:177-240)
+__device__ __forceinline__ bool hit_quad(const DevQuad& q, const double o[3], const double d[3],
+                                         double tmin, double tmax, double& t) {
+    double den = q.n[0] * d[0] + q.n[1] * d[1] + q.n[2] * d[2];
+    if (fabs(den) < 1e-9) return false;
+    double vx = q.v[0] - o[0], vy = q.v[1] - o[1], vz = q.v[2] - o[2];
+    double ht = (q.n[0] * vx + q.n[1] * vy + q.n[2] * vz) / den;
+    if (!(tmin < ht && ht < tmax)) return false;
+    double px = o[0] + d[0] * ht, py = o[1] + d[1] * ht, pz = o[2] + d[2] * ht;
+    double wx = px - q.v[0], wy = py - q.v[1], wz = pz - q.v[2];
+    // alpha = dot(sn, cross(w, s2)); beta = dot(sn, cross(s1, w))
+    double c1x = wy * q.s2[2] - wz * q.s2[1];
+    double c1y = wz * q.s2[0] - wx * q.s2[2];
+    double c1z = wx * q.s2[1] - wy * q.s2[0];
+    double alpha = q.sn[0] * c1x + q.sn[1] * c1y + q.sn[2] * c1z;
+    double c2x = q.s1[1] * wz - q.s1[2] * wy;
+    double c2y = q.s1[2] * wx - q.s1[0] * wz;
+    double c2z = q.s1[0] * wy - q.s1[1] * wx;
+    double beta = q.sn[0] * c2x + q.sn[1] * c2y + q.sn[2] * c2z;
+    if (0 <= alpha && alpha <= 1 && 0 <= beta && beta <= 1) {
+        t = ht;
+        return true;
+    }
+    return false;
+}
+
+// Per-lane traversal stack. LDS: [level][lane] so a wave's pushes hit 64 distinct banks.
+// GLOBAL: the same interleave in an HBM buffer, for trees deeper than the LDS stack.
+template <int SD, bool GLOBAL>
+struct Stack {
+    uint32_t* base;
+    uint32_t stride;
+    __device__ __forceinline__ void put(int i, uint32_t v) { base[static_cast<size_t>(i) * stride] = v; }
+    __device__ __forceinline__ uint32_t get(int i) const { return base[static_cast<size_t>(i) * stride]; }
+};
+
+// BVH::hit_by (bvh.h:585-715): iterative DFS over the preorder nodes, near child first by the
+// sign of the ray direction on the split axis, leaf primitives in order shrinking t_max.
+template <int SD, bool GLOBAL, bool COUNT>
+__device__ __forceinline__ bool trace(const SceneView& S, Stack<SD, GLOBAL>& st, const double o[3],
+                                      const double d[3], double tmin, double& tmax,
+                                      uint32_t& hit_ref, Counters& ctr) {
+    const double inv[3] = {1 / d[0], 1 / d[1], 1 / d[2]};
+    const int neg[3] = {d[0] < 0, d[1] < 0, d[2] < 0};
+    const double a = d[0] * d[0] + d[1] * d[1] + d[2] * d[2];  // dot(ray.dir, ray.dir)
+    bool found = false;
+    int sp = 0;
+    uint32_t cur = 0;
+    while (true) {
+        const DevNode& n = S.nodes[cur];
+        if (COUNT) ctr.nodes++;
+        const bool enter = (n.flags & kNodeAlways) || slab(n, o, inv, neg, tmin, tmax);
+        if (enter) {
+            if (n.count > 0) {
+                const uint32_t end = n.index + n.count;
+                for (uint32_t i = n.index; i < end; ++i) {
+                    const uint32_t ref = S.refs[i];
+                    double t;
+                    bool h;
+                    if (ref & kRefQuad) {
+                        if (COUNT) ctr.quad_tests++;
+                        h = hit_quad(S.quads[ref & ~kRefQuad], o, d, tmin, tmax, t);
+                    } else {
+                        if (COUNT) ctr.sphere_tests++;
+                        h = hit_sphere(S.spheres[ref], o, d, a, tmin, tmax, t);
+                    }
+                    if (h) {
+                        tmax = t;
+                        hit_ref = ref;
+                        found = true;
+                    }
+                }
+                if (sp == 0) break;
+                cur = st.get(--sp);
+            } else {
+                if (neg[n.axis]) {
+                    st.put(sp++, cur + 1);
+                    cur = n.index;
+                } else {
+                    st.put(sp++, n.index);
+                    cur = cur + 1;
+                }
+            }
+        } else {
+            if (sp == 0) break;
+            cur = st.get(--sp);
+        }
+    }
+    return found;
+}
+
+// Resolve the hit record (hittable.h:46-71): hit point ray(t), outward normal, front face.
+__device__ __forceinline__ uint32_t hit_record(const SceneView& S, uint32_t ref, const double o[3],
+                                               const double d[3], double t, double p[3],
+                                               double nrm[3], bool& front) {
+    p[0] = o[0] + d[0] * t;
+    p[1] = o[1] + d[1] * t;
+    p[2] = o[2] + d[2] * t;
+    double nx, ny, nz;
+    uint32_t m;
+    if (ref & kRefQuad) {
+        const DevQuad& q = S.quads[ref & ~kRefQuad];
+        nx = q.n[0]; ny = q.n[1]; nz = q.n[2];
+        m = S.quad_mat[ref & ~kRefQuad];
+    } else {
+        const DevSphere& sp = S.spheres[ref];
+        const double ir = 1 / sp.r;  // (hit_point - center) / radius
+        nx = (p[0] - sp.c[0]) * ir;
+        ny = (p[1] - sp.c[1]) * ir;
+        nz = (p[2] - sp.c[2]) * ir;
+        m = S.sphere_mat[ref];
+    }
+    if (d[0] * nx + d[1] * ny + d[2] * nz > 0) {
+        nrm[0] = -nx; nrm[1] = -ny; nrm[2] = -nz;
+        front = false;
+    } else {
+        nrm[0] = nx; nrm[1] = ny; nrm[2] = nz;
+        front = true;
+    }
+    return m;
+}
+
+__device__ __forceinline__ uint32_t owned_row(const Work& w, uint32_t k) {
+    uint32_t blk = k / w.row_block, in = k % w.row_block;
+    return (blk * w.tile_count + w.tile_index) * w.row_block + in;
+}
+
+// One path (camera.h:184-258) with forward radiance accumulation.
+template <int SD, bool GLOBAL, bool COUNT>
+__device__ __forceinline__ void trace_path(const SceneView& S, const CamView& C, Stack<SD, GLOBAL>& st,
+                                           uint32_t row, uint32_t col, uint32_t rng,
+                                           double L[3], Counters& ctr) {
+    // random_ray_through_pixel (camera.h:184-200)
+    double o[3], d[3];
+    if (C.defocus_angle <= 0) {
+        o[0] = C.o[0]; o[1] = C.o[1]; o[2] = C.o[2];
+    } else {  // random_point_in_defocus_disk (camera.h:160-168, vec3d.h:79-85)
+        double vx, vy;
+        do {
+            vx = rnd(rng, -1, 1);
+            vy = rnd(rng, -1, 1);
+        } while (!(vx * vx + vy * vy + 0.0 * 0.0 < 1));
+        o[0] = (C.o[0] + C.ddx[0] * vx) + C.ddy[0] * vy;
+        o[1] = (C.o[1] + C.ddx[1] * vx) + C.ddy[1] * vy;
+        o[2] = (C.o[2] + C.ddx[2] * vx) + C.ddy[2] * vy;
+    }
+    const double fr = static_cast<double>(row), fc = static_cast<double>(col);
+    // a g++ build evaluates the second jitter draw (the pixel_delta_y one) first
+    const double uy = rnd(rng, -0.5, 0.5);
+    const double ux = rnd(rng, -0.5, 0.5);
+    for (int k = 0; k < 3; ++k) {
+        double center = (C.p00[k] + C.pdy[k] * fr) + C.pdx[k] * fc;
+        double sample = (center + C.pdx[k] * ux) + C.pdy[k] * uy;
+        d[k] = sample - o[k];
+    }
+    double T[3] = {1, 1, 1};
+    L[0] = L[1] = L[2] = 0;
+    for (uint32_t depth = C.max_depth; depth > 0; --depth) {
+        if (COUNT) ctr.rays++;
+        double tmax = __builtin_inf();
+        uint32_t ref = 0;
+        if (!trace<SD, GLOBAL, COUNT>(S, st, o, d, C.t_min, tmax, ref, ctr)) {
+            L[0] += T[0] * C.bg[0];
+            L[1] += T[1] * C.bg[1];
+            L[2] += T[2] * C.bg[2];
+            return;
+        }
+        double p[3], n[3];
+        bool front;
+        const uint32_t mi = hit_record(S, ref, o, d, tmax, p, n, front);
+        const DevMaterial& M = S.mats[mi];
+        double nd[3];
+        if (M.kind == CRT_LAMBERTIAN) {  // material.h:64-86
+            double rx, ry, rz;
+            random_unit_vector(rng, rx, ry, rz);
+            nd[0] = n[0] + rx; nd[1] = n[1] + ry; nd[2] = n[2] + rz;
+            if (fabs(nd[0]) < 1e-8 && fabs(nd[1]) < 1e-8 && fabs(nd[2]) < 1e-8) {
+                nd[0] = n[0]; nd[1] = n[1]; nd[2] = n[2];
+            }
+        } else if (M.kind == CRT_METAL) {  // material.h:116-139
+            const double il = 1 / sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
+            const double ux0 = d[0] * il, uy0 = d[1] * il, uz0 = d[2] * il;
+            const double k2 = 2 * (ux0 * n[0] + uy0 * n[1] + uz0 * n[2]);
+            double rx, ry, rz;
+            random_unit_vector(rng, rx, ry, rz);
+            nd[0] = (ux0 - n[0] * k2) + rx * M.param;
+            nd[1] = (uy0 - n[1] * k2) + ry * M.param;
+            nd[2] = (uz0 - n[2] * k2) + rz * M.param;
+            if (n[0] * nd[0] + n[1] * nd[1] + n[2] * nd[2] < 0) return;  // absorbed; emits 0
+        } else if (M.kind == CRT_DIELECTRIC) {  // material.h:185-218, vec3d.h:144-200
+            const double ratio = front ? 1. / M.param : M.param / 1.;
+            const double il = 1 / sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
+            const double ux0 = d[0] * il, uy0 = d[1] * il, uz0 = d[2] * il;
+            const double cosv = fmin((-ux0) * n[0] + (-uy0) * n[1] + (-uz0) * n[2], 1.);
+            const double sinv = sqrt(1 - cosv * cosv);
+            bool reflect;
+            if (ratio * sinv > 1) {
+                reflect = true;  // total internal reflection, no draw
+            } else {
+                double r0 = (1 - ratio) / (1 + ratio);
+                r0 = r0 * r0;
+                const double refl = r0 + (1 - r0) * pow5(1 - cosv);
+                reflect = rnd(rng, 0, 1) < refl;
+            }
+            if (reflect) {
+                const double k2 = 2 * (ux0 * n[0] + uy0 * n[1] + uz0 * n[2]);
+                nd[0] = ux0 - n[0] * k2;
+                nd[1] = uy0 - n[1] * k2;
+                nd[2] = uz0 - n[2] * k2;
+            } else {
+                const double px = (ux0 + n[0] * cosv) * ratio;
+                const double py = (uy0 + n[1] * cosv) * ratio;
+                const double pz = (uz0 + n[2] * cosv) * ratio;
+                const double s = -sqrt(fabs(1 - (px * px + py * py + pz * pz)));
+                nd[0] = px + n[0] * s;
+                nd[1] = py + n[1] * s;
+                nd[2] = pz + n[2] * s;
+            }
+        } else {  // DiffuseLight: emits, never scatters (material.h:248-263)
+            L[0] += T[0] * M.emit[0];
+            L[1] += T[1] * M.emit[1];
+            L[2] += T[2] * M.emit[2];
+            return;
+        }
+        if (M.kind != CRT_DIELECTRIC) {  // attenuation = intrinsic colour (dielectric: 1)
+            T[0] = T[0] * M.color[0];
+            T[1] = T[1] * M.color[1];
+            T[2] = T[2] * M.color[2];
+        }
+        o[0] = p[0]; o[1] = p[1]; o[2] = p[2];
+        d[0] = nd[0]; d[1] = nd[1]; d[2] = nd[2];
+    }
+    // depth exhausted: ray_color returns RGB::zero() (camera.h:211-213)
+}
+
+// The render kernel. Thread -> (sample chunk, pixel); each wave owns one 8x8 pixel tile so
+// primary rays of a wave are coherent. Each thread sums its chunk's samples in sample order into
+// partial[chunk][pixel].
+template <int SD, bool GLOBAL, bool COUNT>
+__global__ __launch_bounds__(kBlock) void render_kernel(SceneView S, CamView C, Work W,
+                                                        double* __restrict__ partial,
+                                                        uint32_t* __restrict__ gstack,
+                                                        Counters* __restrict__ counters) {
+    __shared__ uint32_t lstack[GLOBAL ? 1 : SD * kBlock];
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t wave = (static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x) >> 6;
+    const uint32_t chunk = static_cast<uint32_t>(wave / W.tiles);
+    const uint32_t tile = static_cast<uint32_t>(wave % W.tiles);
+    Counters ctr{0, 0, 0, 0};
+    if (chunk < W.chunks) {
+        const uint32_t tx = tile % W.tiles_x, ty = tile / W.tiles_x;
+        const uint32_t col = tx * 8 + (lane & 7);
+        const uint32_t k = ty * 8 + (lane >> 3);
+        if (col < C.w && k < W.owned_rows) {
+            const uint32_t row = owned_row(W, k);
+            Stack<SD, GLOBAL> st;
+            if (GLOBAL) {
+                const uint32_t stride = gridDim.x * kBlock;
+                st.base = gstack + (static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x);
+                st.stride = stride;
+            } else {
+                st.base = lstack + threadIdx.x;
+                st.stride = kBlock;
+            }
+            const uint32_t pixel = row * C.w + col;
+            const uint32_t s0 = chunk * W.chunk_len;
+            const uint32_t s1 = min(C.spp, s0 + W.chunk_len);
+            double acc[3] = {0, 0, 0};
+            for (uint32_t s = s0; s < s1; ++s) {
+                double L[3];
+                trace_path<SD, GLOBAL, COUNT>(S, C, st, row, col, sample_seed(C.base_seed, pixel, s),
+                                              L, ctr);
+                acc[0] = acc[0] + L[0];
+                acc[1] = acc[1] + L[1];
+                acc[2] = acc[2] + L[2];
+            }
+            if (!COUNT) {
+                double* dst = partial + (static_cast<size_t>(chunk) * C.h * C.w + pixel) * 3;
+                dst[0] = acc[0];
+                dst[1] = acc[1];
+                dst[2] = acc[2];
+            }
+        }
+    }
+    if (COUNT) {
+        atomicAdd(&counters->rays, ctr.rays);
+        atomicAdd(&counters->nodes, ctr.nodes);
+        atomicAdd(&counters->sphere_tests, ctr.sphere_tests);
+        atomicAdd(&counters->quad_tests, ctr.quad_tests);
+    }
+}
+
+// pixel_color /= spp (camera.h:290, rgb.h:76): sum the chunks in order, multiply by 1/spp.
+__global__ __launch_bounds__(256) void resolve_kernel(const double* __restrict__ partial,
+                                                      double* __restrict__ out, Work W, uint32_t w,
+                                                      uint32_t h, double inv_spp) {
+    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * 256 + threadIdx.x;
+    if (i >= static_cast<uint64_t>(W.owned_rows) * w) return;
+    const uint32_t k = static_cast<uint32_t>(i / w), col = static_cast<uint32_t>(i % w);
+    const uint32_t row = owned_row(W, k);
+    const size_t pix = static_cast<size_t>(row) * w + col;
+    const size_t plane = static_cast<size_t>(h) * w * 3;
+    double r = partial[pix * 3 + 0], g = partial[pix * 3 + 1], b = partial[pix * 3 + 2];
+    for (uint32_t c = 1; c < W.chunks; ++c) {
+        r = r + partial[c * plane + pix * 3 + 0];
+        g = g + partial[c * plane + pix * 3 + 1];
+        b = b + partial[c * plane + pix * 3 + 2];
+    }
+    out[pix * 3 + 0] = r * inv_spp;
+    out[pix * 3 + 1] = g * inv_spp;
+    out[pix * 3 + 2] = b * inv_spp;
+}
+
+// Closest-hit queries (BVH::hit_by for an arbitrary ray batch).
+__global__ __launch_bounds__(kBlock) void hits_kernel(SceneView S, const double* __restrict__ rays,
+                                                      uint32_t n, double t_min, double t_max,
+                                                      const uint32_t* __restrict__ ref_prim,
+                                                      uint32_t num_spheres,
+                                                      crt_hit* __restrict__ out,
+                                                      uint32_t* __restrict__ gstack) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    Stack<0, true> st;
+    st.base = gstack + i;
+    st.stride = gridDim.x * kBlock;
+    double o[3] = {rays[6 * i + 0], rays[6 * i + 1], rays[6 * i + 2]};
+    double d[3] = {rays[6 * i + 3], rays[6 * i + 4], rays[6 * i + 5]};
+    double tmax = t_max;
+    uint32_t ref = 0;
+    Counters ctr{};
+    crt_hit h{};
+    h.prim = -1;
+    if (trace<0, true, false>(S, st, o, d, t_min, tmax, ref, ctr)) {
+        double p[3], nrm[3];
+        bool front;
+        h.material = hit_record(S, ref, o, d, tmax, p, nrm, front);
+        h.t = tmax;
+        for (int k = 0; k < 3; ++k) { h.point[k] = p[k]; h.normal[k] = nrm[k]; }
+        h.front_face = front ? 1 : 0;
+        // ref_prim: spheres at [0, num_spheres), parallelograms after them
+        const uint32_t k = (ref & kRefQuad) ? num_spheres + (ref & ~kRefQuad) : ref;
+        h.prim = static_cast<int32_t>(ref_prim[k]);
+    }
+    out[i] = h;
+}
+
+}  // namespace dev
+
+// =============================================================================================
+// host launch plumbing
+
+static dev::SceneView view_of(const DeviceCopy& c) {
+    return dev::SceneView{c.nodes, c.refs, c.spheres, c.sphere_mat, c.quads, c.quad_mat, c.mats};
+}
+
+int device_count(int* n) {
+    hipError_t e = hipGetDeviceCount(n);
+    if (e != hipSuccess) {
+        *n = 0;
+        return fail(CRT_E_NODEVICE, std::string("hipGetDeviceCount: ") + hipGetErrorString(e));
+    }
+    return CRT_OK;
+}
+
+static int check_device(int device) {
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n == 0)
+        return fail(CRT_E_NODEVICE, "no HIP device visible (the render path has no CPU fallback)");
+    if (device < 0 || device >= n || device >= kMaxDevices)
+        return fail(CRT_E_NODEVICE, "device " + std::to_string(device) + " out of range");
+    return CRT_OK;
+}
+
+struct DeviceGuard {
+    int prev = 0;
+    explicit DeviceGuard(int d) { (void)hipGetDevice(&prev); (void)hipSetDevice(d); }
+    ~DeviceGuard() { (void)hipSetDevice(prev); }
+};
+
+static size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
+
+int device_upload(crt_scene* s, int device) {
+    int rc = check_device(device);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> lk(s->mu);
+    DeviceCopy& c = s->dev[device];
+    if (c.valid) return CRT_OK;
+    DeviceGuard g(device);
+    // one allocation, sub-arrays 256-byte aligned; slot refs stored twice: refs, then the
+    // ref -> primitive map the hit queries report with.
+    const size_t n_nodes = s->dnodes.size(), n_refs = s->refs.size();
+    const size_t n_sp = s->spheres.size(), n_q = s->quads.size(), n_m = s->dmats.size();
+    size_t off_nodes = 0;
+    size_t off_refs = align256(off_nodes + n_nodes * sizeof(DevNode));
+    size_t off_sp = align256(off_refs + n_refs * 4);
+    size_t off_spm = align256(off_sp + n_sp * sizeof(DevSphere));
+    size_t off_q = align256(off_spm + n_sp * 4);
+    size_t off_qm = align256(off_q + n_q * sizeof(DevQuad));
+    size_t off_m = align256(off_qm + n_q * 4);
+    size_t total = align256(off_m + std::max<size_t>(1, n_m) * sizeof(DevMaterial));
+    void* base = nullptr;
+    HIP_TRY(hipMalloc(&base, total));
+    char* b = static_cast<char*>(base);
+    auto up = [&](size_t off, const void* src, size_t bytes) -> hipError_t {
+        if (!bytes) return hipSuccess;
+        return hipMemcpy(b + off, src, bytes, hipMemcpyHostToDevice);
+    };
+    hipError_t e = hipSuccess;
+    if (e == hipSuccess) e = up(off_nodes, s->dnodes.data(), n_nodes * sizeof(DevNode));
+    if (e == hipSuccess) e = up(off_refs, s->refs.data(), n_refs * 4);
+    if (e == hipSuccess) e = up(off_sp, s->spheres.data(), n_sp * sizeof(DevSphere));
+    if (e == hipSuccess) e = up(off_spm, s->sphere_mat.data(), n_sp * 4);
+    if (e == hipSuccess) e = up(off_q, s->quads.data(), n_q * sizeof(DevQuad));
+    if (e == hipSuccess) e = up(off_qm, s->quad_mat.data(), n_q * 4);
+    if (e == hipSuccess) e = up(off_m, s->dmats.data(), n_m * sizeof(DevMaterial));
+    if (e != hipSuccess) {
+        (void)hipFree(base);
+        return fail(CRT_E_HIP, std::string("scene upload: ") + hipGetErrorString(e));
+    }
+    c.base = base;
+    c.bytes = total;
+    c.nodes = reinterpret_cast<DevNode*>(b + off_nodes);
+    c.refs = reinterpret_cast<uint32_t*>(b + off_refs);
+    c.spheres = reinterpret_cast<DevSphere*>(b + off_sp);
+    c.sphere_mat = reinterpret_cast<uint32_t*>(b + off_spm);
+    c.quads = reinterpret_cast<DevQuad*>(b + off_q);
+    c.quad_mat = reinterpret_cast<uint32_t*>(b + off_qm);
+    c.mats = reinterpret_cast<DevMaterial*>(b + off_m);
+    c.valid = true;
+    return CRT_OK;
+}
+
+void device_release(crt_scene* s) {
+    for (int d = 0; d < kMaxDevices; ++d) {
+        DeviceCopy& c = s->dev[d];
+        if (!c.valid) continue;
+        DeviceGuard g(d);
+        (void)hipFree(c.base);
+        c = DeviceCopy{};
+    }
+}
+
+static dev::CamView cam_view(const crt_camera* cam) {
+    dev::CamView v{};
+    for (int k = 0; k < 3; ++k) {
+        v.o[k] = cam->origin[k];
+        v.p00[k] = cam->pixel00[k];
+        v.pdx[k] = cam->pixel_delta_x[k];
+        v.pdy[k] = cam->pixel_delta_y[k];
+        v.ddx[k] = cam->defocus_disk_x[k];
+        v.ddy[k] = cam->defocus_disk_y[k];
+        v.bg[k] = cam->background[k];
+    }
+    v.defocus_angle = cam->defocus_angle;
+    v.t_min = cam->t_min;
+    v.inv_spp = 1 / static_cast<double>(cam->samples_per_pixel);
+    v.w = cam->image_w;
+    v.h = cam->image_h;
+    v.spp = cam->samples_per_pixel;
+    v.max_depth = cam->max_depth;
+    v.base_seed = cam->base_seed;
+    return v;
+}
+
+static uint32_t count_owned(uint32_t h, uint32_t rb, uint32_t tc, uint32_t ti) {
+    uint32_t n = 0;
+    for (uint32_t r = 0; r < h; ++r)
+        if ((r / rb) % tc == ti) ++n;
+    return n;
+}
+
+// resident threads of the render kernel on this device (for the sample-chunk split)
+template <int SD, bool GLOBAL>
+static size_t resident_threads(int device) {
+    static size_t cached[kMaxDevices] = {};
+    if (cached[device]) return cached[device];
+    int blocks = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &blocks, reinterpret_cast<const void*>(dev::render_kernel<SD, GLOBAL, false>),
+            dev::kBlock, 0) != hipSuccess ||
+        blocks <= 0)
+        blocks = 2;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
+        cus = 256;
+    cached[device] = static_cast<size_t>(blocks) * cus * dev::kBlock;
+    return cached[device];
+}
+
+template <int SD, bool GLOBAL>
+static int launch_render(const crt_scene* s, int device, const crt_camera* cam, const dev::Work& w0,
+                         double* d_rgb, hipStream_t stream, crt_render_stats* count_stats) {
+    const DeviceCopy& c = s->dev[device];
+    dev::Work W = w0;
+    const uint64_t pixels = static_cast<uint64_t>(W.owned_rows) * cam->image_w;
+    const size_t resident = resident_threads<SD, GLOBAL>(device);
+    // enough threads for ~8 waves of residency so block-level dynamic dispatch balances rows of
+    // very different cost; never split below 1 sample per thread
+    uint64_t want = (8 * static_cast<uint64_t>(resident) + pixels - 1) / std::max<uint64_t>(1, pixels);
+    W.chunks = static_cast<uint32_t>(std::min<uint64_t>(std::max<uint64_t>(1, want), cam->samples_per_pixel));
+    W.chunk_len = (cam->samples_per_pixel + W.chunks - 1) / W.chunks;
+    W.chunks = (cam->samples_per_pixel + W.chunk_len - 1) / W.chunk_len;
+    const uint64_t waves = static_cast<uint64_t>(W.tiles) * W.chunks;
+    const uint64_t blocks = (waves * 64 + dev::kBlock - 1) / dev::kBlock;
+    if (blocks > 0x7fffffffull) return fail(CRT_E_INVALID, "frame too large for one launch");
+    const size_t plane = static_cast<size_t>(cam->image_h) * cam->image_w * 3;
+
+    double* partial = nullptr;
+    uint32_t* gstack = nullptr;
+    dev::Counters* ctr = nullptr;
+    const bool count = count_stats != nullptr;
+    if (!count) HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&partial), plane * W.chunks * sizeof(double), stream));
+    if (GLOBAL) {
+        size_t bytes = static_cast<size_t>(s->depth + 1) * blocks * dev::kBlock * 4;
+        HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&gstack), bytes, stream));
+    }
+    if (count) {
+        HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&ctr), sizeof(dev::Counters), stream));
+        HIP_TRY(hipMemsetAsync(ctr, 0, sizeof(dev::Counters), stream));
+    }
+    dev::SceneView S = view_of(c);
+    dev::CamView C = cam_view(cam);
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (count) {
+        HIP_TRY(hipEventCreate(&e0));
+        HIP_TRY(hipEventCreate(&e1));
+        HIP_TRY(hipEventRecord(e0, stream));
+        hipLaunchKernelGGL((dev::render_kernel<SD, GLOBAL, true>), dim3(static_cast<uint32_t>(blocks)),
+                           dim3(dev::kBlock), 0, stream, S, C, W, partial, gstack, ctr);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipEventRecord(e1, stream));
+    } else {
+        hipLaunchKernelGGL((dev::render_kernel<SD, GLOBAL, false>), dim3(static_cast<uint32_t>(blocks)),
+                           dim3(dev::kBlock), 0, stream, S, C, W, partial, gstack, ctr);
+        HIP_TRY(hipGetLastError());
+        const uint64_t n = pixels;
+        const uint32_t rb = static_cast<uint32_t>((n + 255) / 256);
+        if (rb) {
+            hipLaunchKernelGGL(dev::resolve_kernel, dim3(rb), dim3(256), 0, stream, partial, d_rgb,
+                               W, cam->image_w, cam->image_h, C.inv_spp);
+            HIP_TRY(hipGetLastError());
+        }
+    }
+    if (partial) HIP_TRY(hipFreeAsync(partial, stream));
+    if (gstack) HIP_TRY(hipFreeAsync(gstack, stream));
+    if (count) {
+        dev::Counters h{};
+        HIP_TRY(hipMemcpyAsync(&h, ctr, sizeof h, hipMemcpyDeviceToHost, stream));
+        HIP_TRY(hipStreamSynchronize(stream));
+        HIP_TRY(hipFreeAsync(ctr, stream));
+        float ms = 0;
+        HIP_TRY(hipEventElapsedTime(&ms, e0, e1));
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+        count_stats->samples = pixels * cam->samples_per_pixel;
+        count_stats->rays = h.rays;
+        count_stats->nodes_visited = h.nodes;
+        count_stats->sphere_tests = h.sphere_tests;
+        count_stats->parallelogram_tests = h.quad_tests;
+        count_stats->kernel_ms = ms;
+    }
+    return CRT_OK;
+}
+
+int device_render(const crt_scene* s, int device, const crt_camera* cam, const crt_tiling* t,
+                  double* d_rgb, void* stream, crt_render_stats* count_stats) {
+    int rc = check_device(device);
+    if (rc) return rc;
+    if (!s->dev[device].valid)
+        return fail(CRT_E_NOT_UPLOADED, "scene not uploaded to device " + std::to_string(device));
+    if (cam->image_w == 0 || cam->image_h == 0) return fail(CRT_E_INVALID, "empty image");
+    if (static_cast<uint64_t>(cam->image_w) * cam->image_h >= 0xffffffffull)
+        return fail(CRT_E_INVALID, "image has more than 2^32-1 pixels");
+    crt_tiling tl{1, 1, 0, 0};
+    if (t) tl = *t;
+    if (tl.row_block == 0 || tl.tile_count == 0 || tl.tile_index >= tl.tile_count)
+        return fail(CRT_E_INVALID, "bad tiling");
+    DeviceGuard g(device);
+    dev::Work W{};
+    W.row_block = tl.row_block;
+    W.tile_count = tl.tile_count;
+    W.tile_index = tl.tile_index;
+    W.owned_rows = count_owned(cam->image_h, tl.row_block, tl.tile_count, tl.tile_index);
+    if (W.owned_rows == 0 || cam->samples_per_pixel == 0) {
+        if (count_stats) *count_stats = crt_render_stats{};
+        if (cam->samples_per_pixel == 0 && d_rgb && W.owned_rows) {
+            // 0 spp: the reference multiplies a zero sum by 1/0 -> NaN (0 * inf)
+            std::vector<double> nanrow(static_cast<size_t>(cam->image_w) * 3,
+                                       std::numeric_limits<double>::quiet_NaN());
+            for (uint32_t k = 0; k < W.owned_rows; ++k) {
+                uint32_t blk = k / W.row_block, in = k % W.row_block;
+                uint32_t row = (blk * W.tile_count + W.tile_index) * W.row_block + in;
+                HIP_TRY(hipMemcpyAsync(d_rgb + static_cast<size_t>(row) * cam->image_w * 3, nanrow.data(),
+                                       nanrow.size() * 8, hipMemcpyHostToDevice,
+                                       static_cast<hipStream_t>(stream)));
+            }
+            HIP_TRY(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+        }
+        return CRT_OK;
+    }
+    W.tiles_x = (cam->image_w + 7) / 8;
+    W.tiles_y = (W.owned_rows + 7) / 8;
+    W.tiles = W.tiles_x * W.tiles_y;
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    if (count_stats) HIP_TRY(hipStreamCreate(&st));
+    int r;
+    // stack entries needed <= depth - 1
+    if (s->depth <= 17)
+        r = launch_render<16, false>(s, device, cam, W, d_rgb, st, count_stats);
+    else if (s->depth <= 33)
+        r = launch_render<32, false>(s, device, cam, W, d_rgb, st, count_stats);
+    else
+        r = launch_render<0, true>(s, device, cam, W, d_rgb, st, count_stats);
+    if (count_stats) (void)hipStreamDestroy(st);
+    return r;
+}
+
+int device_closest_hits(crt_scene* s, int device, const double* rays, size_t n, double t_min,
+                        double t_max, crt_hit* out) {
+    int rc = device_upload(s, device);
+    if (rc) return rc;
+    if (n == 0) return CRT_OK;
+    if (n > 0x7fffffffu) return fail(CRT_E_INVALID, "too many rays");
+    DeviceGuard g(device);
+    const DeviceCopy& c = s->dev[device];
+    const uint32_t blocks = static_cast<uint32_t>((n + dev::kBlock - 1) / dev::kBlock);
+    // ref -> primitive index: spheres at [0, nsp), parallelograms at [nsp, nsp + nq)
+    const size_t nsp = s->spheres.size(), nq = s->quads.size();
+    std::vector<uint32_t> ref_prim(std::max<size_t>(1, nsp + nq));
+    for (size_t slot = 0; slot < s->refs.size(); ++slot) {
+        uint32_t r = s->refs[slot];
+        ref_prim[(r & kRefQuad) ? nsp + (r & ~kRefQuad) : r] = s->order[slot];
+    }
+    double* d_rays = nullptr;
+    crt_hit* d_out = nullptr;
+    uint32_t *d_sp = nullptr, *d_stack = nullptr;
+    HIP_TRY(hipMalloc(&d_rays, n * 6 * sizeof(double)));
+    HIP_TRY(hipMalloc(&d_out, n * sizeof(crt_hit)));
+    HIP_TRY(hipMalloc(&d_sp, ref_prim.size() * 4));
+    HIP_TRY(hipMalloc(&d_stack, static_cast<size_t>(s->depth + 1) * blocks * dev::kBlock * 4));
+    HIP_TRY(hipMemcpy(d_rays, rays, n * 6 * sizeof(double), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(d_sp, ref_prim.data(), ref_prim.size() * 4, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(dev::hits_kernel, dim3(blocks), dim3(dev::kBlock), 0, 0, view_of(c), d_rays,
+                       static_cast<uint32_t>(n), t_min, t_max, d_sp, static_cast<uint32_t>(nsp), d_out, d_stack);
+    hipError_t le = hipGetLastError();
+    hipError_t se = hipDeviceSynchronize();
+    if (le == hipSuccess && se == hipSuccess)
+        se = hipMemcpy(out, d_out, n * sizeof(crt_hit), hipMemcpyDeviceToHost);
+    (void)hipFree(d_rays);
+    (void)hipFree(d_out);
+    (void)hipFree(d_sp);
+    (void)hipFree(d_stack);
+    if (le != hipSuccess) return fail(CRT_E_HIP, std::string("hits_kernel launch: ") + hipGetErrorString(le));
+    if (se != hipSuccess) return fail(CRT_E_HIP, std::string("hits_kernel: ") + hipGetErrorString(se));
+    return CRT_OK;
+}
+
+int render_multi(crt_scene* s, const crt_camera* cam, int num_devices, double* h_rgb,
+                 crt_render_stats* stats) {
+    int avail = 0;
+    if (hipGetDeviceCount(&avail) != hipSuccess || avail == 0)
+        return fail(CRT_E_NODEVICE, "no HIP device visible (the render path has no CPU fallback)");
+    if (num_devices <= 0) num_devices = avail;
+    num_devices = std::min(num_devices, std::min(avail, kMaxDevices));
+    const size_t frame = static_cast<size_t>(cam->image_h) * cam->image_w * 3;
+    std::vector<double*> bufs(num_devices, nullptr);
+    std::vector<hipStream_t> streams(num_devices, nullptr);
+    std::vector<hipEvent_t> ev0(num_devices, nullptr), ev1(num_devices, nullptr);
+    const uint32_t rb = 16;
+    int rc = CRT_OK;
+    for (int d = 0; d < num_devices && rc == CRT_OK; ++d) {
+        rc = device_upload(s, d);
+        if (rc) break;
+        DeviceGuard g(d);
+        if (hipStreamCreate(&streams[d]) != hipSuccess ||
+            hipMalloc(&bufs[d], frame * sizeof(double)) != hipSuccess ||
+            hipEventCreate(&ev0[d]) != hipSuccess || hipEventCreate(&ev1[d]) != hipSuccess) {
+            rc = fail(CRT_E_HIP, "render: per-device setup failed on device " + std::to_string(d));
+            break;
+        }
+        crt_tiling t{rb, static_cast<uint32_t>(num_devices), static_cast<uint32_t>(d), 0};
+        (void)hipEventRecord(ev0[d], streams[d]);
+        rc = device_render(s, d, cam, &t, bufs[d], streams[d], nullptr);
+        (void)hipEventRecord(ev1[d], streams[d]);
+    }
+    float max_ms = 0;
+    for (int d = 0; d < num_devices; ++d) {
+        if (!streams[d]) continue;
+        DeviceGuard g(d);
+        hipError_t e = hipStreamSynchronize(streams[d]);
+        if (e != hipSuccess && rc == CRT_OK)
+            rc = fail(CRT_E_HIP, std::string("render on device ") + std::to_string(d) + ": " +
+                                     hipGetErrorString(e));
+        if (rc == CRT_OK) {
+            float ms = 0;
+            (void)hipEventElapsedTime(&ms, ev0[d], ev1[d]);
+            max_ms = std::max(max_ms, ms);
+            // gather the owned row blocks of device d
+            for (uint32_t r0 = static_cast<uint32_t>(d) * rb; r0 < cam->image_h;
+                 r0 += rb * static_cast<uint32_t>(num_devices)) {
+                uint32_t rows = std::min(rb, cam->image_h - r0);
+                size_t off = static_cast<size_t>(r0) * cam->image_w * 3;
+                size_t bytes = static_cast<size_t>(rows) * cam->image_w * 3 * sizeof(double);
+                if (hipMemcpy(h_rgb + off, bufs[d] + off, bytes, hipMemcpyDeviceToHost) != hipSuccess) {
+                    rc = fail(CRT_E_HIP, "render: gather failed");
+                    break;
+                }
+            }
+        }
+    }
+    for (int d = 0; d < num_devices; ++d) {
+        DeviceGuard g(d);
+        if (bufs[d]) (void)hipFree(bufs[d]);
+        if (streams[d]) (void)hipStreamDestroy(streams[d]);
+        if (ev0[d]) (void)hipEventDestroy(ev0[d]);
+        if (ev1[d]) (void)hipEventDestroy(ev1[d]);
+    }
+    if (stats && rc == CRT_OK) {
+        *stats = crt_render_stats{};
+        stats->samples = static_cast<uint64_t>(cam->image_w) * cam->image_h * cam->samples_per_pixel;
+        stats->kernel_ms = max_ms;
+    }
+    return rc;
+}
+
+}  // namespace crt

@@ -1,0 +1,328 @@
+/* TEST INFRASTRUCTURE — builds into oracle/_ref/ only; never shipped, never measured as product.
+ *
+ * Driver that runs the REFERENCE's own code (headers under /root/reference/include, compiled
+ * by g++ like the reference's CMakeLists.txt: -std=c++20 -O3, OpenMP) on scenes serialized in
+ * the CRTS format, to produce golden vectors:
+ *   camera  <scene>                      Camera::init() outputs            (camera.h:87-157)
+ *   bvh     <scene> <out>                BVH node array + primitive order  (bvh.h:754-776)
+ *   render  <scene> <base> <out> [r0 r1 c0 c1]
+ *                                        per-pixel RGB of the per-sample-seeded render
+ *                                        (camera.h:279-293 loop, reference random_ray_through_pixel
+ *                                        and ray_color; state injected per (pixel, sample))
+ *   samples <scene> <base> <out> r0 r1 c0 c1   per-sample RGB of the same crop
+ *   hits    <scene> <rays> <out>         BVH::hit_by closest hits          (bvh.h:585-715)
+ *   time    <scene> <threads> [rows]     unmodified Camera::render timing  (CPU baseline)
+ *   refsum  <scene> <seed>               1-thread unmodified render checksum (shim check)
+ *
+ * The reference's Camera keeps init/random_ray_through_pixel/ray_color private (implicit
+ * `class` access); the driver reaches them by including every standard header first and then
+ * reading the reference headers under `#define class struct`. No reference source is copied.
+ */
+#include <algorithm>
+#include <array>
+#include <atomic>
+#include <chrono>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <iomanip>
+#include <iostream>
+#include <iterator>
+#include <limits>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <numbers>
+#include <numeric>
+#include <optional>
+#include <random>
+#include <span>
+#include <sstream>
+#include <string>
+#include <type_traits>
+#include <utility>
+#include <vector>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#define class struct
+#include "util/rand_util.h"
+#include "base/scene.h"
+#include "base/material.h"
+#include "base/camera.h"
+#include "shapes/shapes.h"
+#undef class
+
+// ---- CRTS scene file (cpp_raytracer_amd/__init__.py SceneData.to_bytes) -------------------
+struct CamSettings {
+    uint32_t w, h, spp, depth;
+    double center[3], direction[3], lookat[3], up[3];
+    double focus_dist, fov, defocus_angle;
+    double background[3];
+    uint32_t has_lookat, has_focus_dist, fov_is_vertical, reserved;
+};
+static_assert(sizeof(CamSettings) == 176);
+struct MatRec { uint32_t kind, reserved; double color[3]; double param; };
+struct ObjRec { uint32_t kind, material; double v[9]; };
+static_assert(sizeof(MatRec) == 40 && sizeof(ObjRec) == 80);
+
+struct Loaded {
+    Scene world;
+    CamSettings cs;
+    std::vector<std::shared_ptr<Material>> mats;
+};
+
+static Loaded load(const char* path) {
+    std::ifstream f(path, std::ios::binary);
+    if (!f) { std::fprintf(stderr, "cannot open %s\n", path); std::exit(2); }
+    char magic[4];
+    uint32_t ver;
+    uint64_t nm, no;
+    f.read(magic, 4);
+    f.read(reinterpret_cast<char*>(&ver), 4);
+    f.read(reinterpret_cast<char*>(&nm), 8);
+    f.read(reinterpret_cast<char*>(&no), 8);
+    if (std::memcmp(magic, "CRTS", 4) || ver != 1) { std::fprintf(stderr, "bad scene\n"); std::exit(2); }
+    Loaded L;
+    f.read(reinterpret_cast<char*>(&L.cs), sizeof L.cs);
+    std::vector<MatRec> m(nm);
+    std::vector<ObjRec> o(no);
+    f.read(reinterpret_cast<char*>(m.data()), nm * sizeof(MatRec));
+    f.read(reinterpret_cast<char*>(o.data()), no * sizeof(ObjRec));
+    for (auto& r : m) {
+        RGB c = RGB::from_mag(r.color[0], r.color[1], r.color[2]);
+        switch (r.kind) {
+            case 1: L.mats.push_back(std::make_shared<Lambertian>(c)); break;
+            case 2: L.mats.push_back(std::make_shared<Metal>(c, r.param)); break;
+            case 3: L.mats.push_back(std::make_shared<Dielectric>(r.param)); break;
+            case 4: L.mats.push_back(std::make_shared<DiffuseLight>(c, r.param)); break;
+            default: std::fprintf(stderr, "bad material\n"); std::exit(2);
+        }
+    }
+    for (auto& r : o) {
+        auto mat = L.mats.at(r.material);
+        Point3D a{r.v[0], r.v[1], r.v[2]}, b{r.v[3], r.v[4], r.v[5]}, c{r.v[6], r.v[7], r.v[8]};
+        switch (r.kind) {
+            case 1: L.world.add(std::make_shared<Sphere>(a, r.v[3], mat)); break;
+            case 2: L.world.add(std::make_shared<Parallelogram>(a, b, c, mat)); break;
+            case 3: L.world.add(std::make_shared<Box>(a, b, mat)); break;
+            default: std::fprintf(stderr, "bad object\n"); std::exit(2);
+        }
+    }
+    return L;
+}
+
+// The reference Camera with the scene's settings. Angles in the file are radians, so they are
+// stored directly (the setters would convert from degrees).
+static Camera make_camera(const CamSettings& s) {
+    Camera cam;
+    cam.set_image_dimensions(s.w, s.h);
+    cam.set_samples_per_pixel(s.spp);
+    cam.set_max_depth(s.depth);
+    cam.set_camera_center(Point3D{s.center[0], s.center[1], s.center[2]});
+    cam.set_camera_direction(Vec3D{s.direction[0], s.direction[1], s.direction[2]});
+    if (s.has_lookat) cam.set_camera_lookat(Point3D{s.lookat[0], s.lookat[1], s.lookat[2]});
+    if (s.has_focus_dist) cam.set_focus_distance(s.focus_dist);
+    cam.set_camera_up_direction(Vec3D{s.up[0], s.up[1], s.up[2]});
+    if (s.fov_is_vertical) { cam.vertical_fov = s.fov; cam.horizontal_fov.reset(); }
+    else { cam.horizontal_fov = s.fov; cam.vertical_fov.reset(); }
+    cam.defocus_angle = s.defocus_angle;
+    cam.set_background(RGB::from_mag(s.background[0], s.background[1], s.background[2]));
+    return cam;
+}
+
+// per-(pixel, sample) seed: the framework's fixed hash (crt_sample_seed in include/crt_render.h)
+static uint32_t sample_seed(uint32_t base, uint32_t pixel, uint32_t sample) {
+    uint64_t z = (static_cast<uint64_t>(pixel) << 32) | sample;
+    z += static_cast<uint64_t>(base) * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    return static_cast<uint32_t>(z ^ (z >> 32));
+}
+
+static void write_npy(const char* path, const std::vector<double>& data, std::vector<size_t> shape) {
+    std::ostringstream h;
+    h << "{'descr': '<f8', 'fortran_order': False, 'shape': (";
+    for (size_t i = 0; i < shape.size(); ++i) h << shape[i] << (shape.size() == 1 ? "," : (i + 1 < shape.size() ? ", " : ""));
+    h << "), }";
+    std::string hs = h.str();
+    size_t total = 10 + hs.size() + 1;
+    hs += std::string((64 - total % 64) % 64, ' ') + "\n";
+    std::ofstream f(path, std::ios::binary);
+    f.write("\x93NUMPY\x01\x00", 8);
+    uint16_t hl = static_cast<uint16_t>(hs.size());
+    f.write(reinterpret_cast<const char*>(&hl), 2);
+    f.write(hs.data(), hs.size());
+    f.write(reinterpret_cast<const char*>(data.data()), data.size() * sizeof(double));
+}
+
+#ifdef CRT_ORACLE_SHIM
+// per-sample-seeded render of rows [r0,r1) x cols [c0,c1); samples != null -> per-sample RGB
+static void render_crop(Loaded& L, uint32_t base, size_t r0, size_t r1, size_t c0, size_t c1,
+                        std::vector<double>& out, std::vector<double>* samples) {
+    Camera cam = make_camera(L.cs);
+    cam.init();
+    BVH bvh(L.world);
+    const size_t w = c1 - c0, spp = cam.samples_per_pixel;
+    out.assign((r1 - r0) * w * 3, 0.0);
+    if (samples) samples->assign((r1 - r0) * w * spp * 3, 0.0);
+#pragma omp parallel for schedule(dynamic)
+    for (size_t row = r0; row < r1; ++row) {
+        for (size_t col = c0; col < c1; ++col) {
+            auto px = RGB::zero();
+            const uint32_t pixel = static_cast<uint32_t>(row * cam.image_w + col);
+            for (size_t s = 0; s < spp; ++s) {
+                crt_oracle_set_state(sample_seed(base, pixel, static_cast<uint32_t>(s)));
+                auto ray = cam.random_ray_through_pixel(row, col);
+                auto c = cam.ray_color(ray, cam.max_depth, bvh);
+                if (samples) {
+                    double* d = samples->data() + (((row - r0) * w + (col - c0)) * spp + s) * 3;
+                    d[0] = c.r; d[1] = c.g; d[2] = c.b;
+                }
+                px += c;
+            }
+            px /= static_cast<double>(spp);
+            double* d = out.data() + ((row - r0) * w + (col - c0)) * 3;
+            d[0] = px.r; d[1] = px.g; d[2] = px.b;
+        }
+    }
+}
+#endif
+
+int main(int argc, char** argv) {
+    std::ios::sync_with_stdio(true);
+    if (argc < 3) { std::fprintf(stderr, "usage: see header\n"); return 2; }
+    std::string mode = argv[1];
+    // the reference prints progress bars and BVH stats on stdout; keep our own output on fd 3
+    // by writing results to files, and send the reference's chatter to stderr.
+    std::cout.rdbuf(std::cerr.rdbuf());
+    Loaded L = load(argv[2]);
+    if (mode == "camera") {
+        Camera cam = make_camera(L.cs);
+        cam.init();
+        auto pr = [](const char* k, const Vec3D& v) {
+            std::printf("%s %.17g %.17g %.17g\n", k, v.x, v.y, v.z);
+        };
+        pr("origin", cam.camera.origin);
+        pr("pixel00", cam.pixel00_loc);
+        pr("pixel_delta_x", cam.pixel_delta_x);
+        pr("pixel_delta_y", cam.pixel_delta_y);
+        pr("defocus_disk_x", cam.defocus_disk_x);
+        pr("defocus_disk_y", cam.defocus_disk_y);
+        std::printf("size %zu %zu\n", cam.image_w, cam.image_h);
+        return 0;
+    }
+    if (mode == "bvh") {
+        BVH bvh(L.world);
+        auto prims = L.world.get_primitive_components();
+        std::map<const Hittable*, uint32_t> idx;
+        for (size_t i = 0; i < prims.size(); ++i) idx[prims[i].get()] = static_cast<uint32_t>(i);
+        std::ofstream f(argv[3], std::ios::binary);
+        uint64_t nn = bvh.linear_bvh_nodes.size(), np = bvh.primitives.size();
+        f.write(reinterpret_cast<const char*>(&nn), 8);
+        f.write(reinterpret_cast<const char*>(&np), 8);
+        for (auto& n : bvh.linear_bvh_nodes) {
+            double b[6] = {n.aabb.x.min, n.aabb.x.max, n.aabb.y.min, n.aabb.y.max, n.aabb.z.min, n.aabb.z.max};
+            f.write(reinterpret_cast<const char*>(b), sizeof b);
+            uint32_t rec[4] = {static_cast<uint32_t>(n.num_primitives ? n.first_primitive_index : n.second_child_index),
+                               static_cast<uint32_t>(n.num_primitives),
+                               static_cast<uint32_t>(n.num_primitives ? 0 : n.split_axis), 0};
+            f.write(reinterpret_cast<const char*>(rec), sizeof rec);
+        }
+        for (auto& p : bvh.primitives) {
+            uint32_t i = idx.at(p.get());
+            f.write(reinterpret_cast<const char*>(&i), 4);
+        }
+        return 0;
+    }
+#ifdef CRT_ORACLE_SHIM
+    if (mode == "render" || mode == "samples") {
+        uint32_t base = static_cast<uint32_t>(std::strtoul(argv[3], nullptr, 10));
+        size_t r0 = 0, r1 = L.cs.h, c0 = 0, c1 = L.cs.w;
+        if (argc >= 9) {
+            r0 = std::strtoul(argv[5], nullptr, 10); r1 = std::strtoul(argv[6], nullptr, 10);
+            c0 = std::strtoul(argv[7], nullptr, 10); c1 = std::strtoul(argv[8], nullptr, 10);
+        }
+        std::vector<double> out, smp;
+        render_crop(L, base, r0, r1, c0, c1, out, mode == "samples" ? &smp : nullptr);
+        if (mode == "render") write_npy(argv[4], out, {r1 - r0, c1 - c0, 3});
+        else write_npy(argv[4], smp, {r1 - r0, c1 - c0, L.cs.spp, 3});
+        return 0;
+    }
+    if (mode == "hits") {
+        std::vector<char> raw;
+        {
+            std::ifstream g(argv[3], std::ios::binary);
+            raw.assign(std::istreambuf_iterator<char>(g), {});
+        }
+        size_t n = raw.size() / (6 * sizeof(double));
+        const double* r = reinterpret_cast<const double*>(raw.data());
+        BVH bvh(L.world);
+        auto prims = L.world.get_primitive_components();
+        std::map<const Hittable*, uint32_t> idx;
+        for (size_t i = 0; i < prims.size(); ++i) idx[prims[i].get()] = static_cast<uint32_t>(i);
+        // output per ray: t, point[3], normal[3], prim (as double), front (as double)
+        std::vector<double> out(n * 9, 0.0);
+        for (size_t i = 0; i < n; ++i) {
+            Ray3D ray{Point3D{r[6 * i], r[6 * i + 1], r[6 * i + 2]}, Vec3D{r[6 * i + 3], r[6 * i + 4], r[6 * i + 5]}};
+            // identify the primitive by re-running each leaf primitive is not possible from
+            // hit_info; compare hit_info fields and the material pointer instead
+            auto h = bvh.hit_by(ray, Interval::with_min(0.00001));
+            double* o = out.data() + 9 * i;
+            if (!h) { o[7] = -1; continue; }
+            o[0] = h->hit_time;
+            o[1] = h->hit_point.x; o[2] = h->hit_point.y; o[3] = h->hit_point.z;
+            o[4] = h->unit_surface_normal.x; o[5] = h->unit_surface_normal.y; o[6] = h->unit_surface_normal.z;
+            // which primitive: the one whose material pointer and hit time reproduce the hit
+            o[7] = -2;
+            for (size_t p = 0; p < prims.size(); ++p) {
+                auto hp = prims[p]->hit_by(ray, Interval(0.00001, std::numeric_limits<double>::infinity()));
+                if (hp && hp->hit_time == h->hit_time && hp->material == h->material) { o[7] = static_cast<double>(p); break; }
+            }
+            o[8] = h->hit_from_outside ? 1 : 0;
+        }
+        write_npy(argv[4], out, {n, 9});
+        return 0;
+    }
+#endif
+    if (mode == "time") {
+        // Unmodified reference render (its own per-thread RNG seeding), timed; stdout of the
+        // reference goes to stderr. rows (optional) limits the image height (a band).
+        int threads = std::atoi(argv[3]);
+#ifdef _OPENMP
+        omp_set_num_threads(threads);
+#endif
+        SeedSeqGenerator::get_instance().set_seed(12345);
+        Camera cam = make_camera(L.cs);
+        auto t0 = std::chrono::steady_clock::now();
+        auto img = cam.render(L.world);
+        auto t1 = std::chrono::steady_clock::now();
+        double sum = 0;
+        for (size_t r = 0; r < img.height(); ++r)
+            for (size_t c = 0; c < img.width(); ++c) sum += img[r][c].r + img[r][c].g + img[r][c].b;
+        double secs = std::chrono::duration<double>(t1 - t0).count();
+        std::printf("{\"seconds\": %.6f, \"samples\": %zu, \"threads\": %d, \"checksum\": %.17g}\n", secs,
+                    static_cast<size_t>(L.cs.w) * L.cs.h * L.cs.spp, threads, sum);
+        return 0;
+    }
+    if (mode == "refsum") {
+#ifdef _OPENMP
+        omp_set_num_threads(1);
+#endif
+        SeedSeqGenerator::get_instance().set_seed(static_cast<uint32_t>(std::strtoul(argv[3], nullptr, 10)));
+        Camera cam = make_camera(L.cs);
+        auto img = cam.render(L.world);
+        double sum = 0;
+        for (size_t r = 0; r < img.height(); ++r)
+            for (size_t c = 0; c < img.width(); ++c) sum += img[r][c].r + img[r][c].g + img[r][c].b;
+        std::printf("%.17g\n", sum);
+        return 0;
+    }
+    std::fprintf(stderr, "unknown mode %s\n", mode.c_str());
+    return 2;
+}

@@ -1,0 +1,142 @@
+"""Regenerate the golden fixtures of tests/golden/ from the REFERENCE's own code.
+
+Runs only in a container that has /root/reference (the GPU box does not): builds
+oracle/_ref/ref_driver (reference headers + RNG instrumentation shim, see oracle/Makefile), writes
+the scenes as CRTS files with the library's named-scene builders, and asks the reference code for
+  * Camera::init outputs            -> cameras.json
+  * BVH node arrays + prim order    -> bvh_<scene>.npz
+  * per-sample-seeded renders       -> render_<case>.npz  (per-pixel RGB, float64)
+  * per-sample radiance             -> samples_<case>.npz
+  * closest-hit records             -> hits_<scene>.npz
+Fixtures hold inputs and expected outputs only. Usage: python tests/golden/gen_golden.py
+"""
+from __future__ import annotations
+
+import hashlib
+import json
+import subprocess
+import sys
+import tempfile
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[2]
+sys.path.insert(0, str(ROOT))
+import cpp_raytracer_amd as crt  # noqa: E402
+from cpp_raytracer_amd import camera_with  # noqa: E402
+
+GOLD = Path(__file__).resolve().parent
+REF = ROOT / "oracle" / "_ref" / "ref_driver"
+
+# (case, scene, seed, camera overrides, base_seed, crop (r0, r1, c0, c1) or None)
+RENDER_CASES = [
+    ("config1", "config1", None, {}, 7, None),
+    ("rtow_crop", "rtow_final", 42, dict(image_w=1200, image_h=800, samples_per_pixel=8, max_depth=50),
+     11, (360, 424, 560, 624)),
+    ("rtow_glass_crop", "rtow_final", 42, dict(image_w=1200, image_h=800, samples_per_pixel=16, max_depth=50),
+     12, (330, 362, 580, 644)),
+    ("cornell_crop", "cornell", None, dict(image_w=600, image_h=600, samples_per_pixel=4, max_depth=1000),
+     13, (250, 314, 200, 264)),
+    ("cornell_empty_small", "cornell_empty", None, dict(image_w=40, image_h=40, samples_per_pixel=8, max_depth=50),
+     14, None),
+    ("parallelograms_small", "parallelograms", None, dict(image_w=48, image_h=48, samples_per_pixel=4),
+     15, None),
+    ("lights_crop", "rtow_final_lights", None, dict(image_w=400, image_h=225, samples_per_pixel=16),
+     16, (80, 112, 180, 244)),
+    ("christmas_crop", "christmas_tree", None, dict(image_w=270, image_h=152, samples_per_pixel=8),
+     17, (40, 72, 110, 174)),
+]
+SAMPLE_CASES = [
+    ("rtow_samples", "rtow_final", 42, dict(image_w=1200, image_h=800, samples_per_pixel=16, max_depth=50),
+     21, (392, 400, 592, 600)),
+    ("cornell_samples", "cornell", None, dict(image_w=600, image_h=600, samples_per_pixel=16, max_depth=1000),
+     22, (296, 304, 296, 304)),
+]
+BVH_SCENES = [("config1", None), ("rtow_final", 42), ("cornell", None), ("parallelograms", None),
+              ("christmas_tree", None), ("bvh_pathological", None), ("rtow_final_lights", None)]
+HIT_SCENES = [("rtow_final", 42, 4096), ("cornell", None, 4096), ("christmas_tree", None, 2048)]
+
+
+def scene_file(tmp: Path, name: str, seed, overrides: dict) -> tuple[Path, crt.SceneData]:
+    d = crt.SceneData.named(name, seed)
+    d.camera = camera_with(d.camera, **overrides)
+    p = tmp / f"{name}_{abs(hash(json.dumps(overrides, sort_keys=True)))}.crts"
+    d.save(p)
+    return p, d
+
+
+def run(*args) -> str:
+    r = subprocess.run([str(REF), *map(str, args)], check=True, capture_output=True, text=True)
+    return r.stdout
+
+
+def scene_digest(d: crt.SceneData) -> str:
+    return hashlib.sha256(d.materials.tobytes() + d.objects.tobytes()).hexdigest()
+
+
+def main() -> None:
+    subprocess.run(["make", "-C", str(ROOT / "oracle"), "ref"], check=True)
+    meta = {"generator": "tests/golden/gen_golden.py", "reference": "DeltaPavonis/cpp_raytracer (oracle/_ref)",
+            "scenes": {}, "renders": {}, "cameras": {}}
+    with tempfile.TemporaryDirectory() as td:
+        tmp = Path(td)
+        # scenes + cameras + BVHs
+        for name, seed in BVH_SCENES:
+            p, d = scene_file(tmp, name, seed, {})
+            meta["scenes"][name] = {"seed": seed, "objects": int(len(d.objects)),
+                                    "materials": int(len(d.materials)), "sha256": scene_digest(d)}
+            cam = {}
+            for line in run("camera", p).splitlines():
+                k, *vals = line.split()
+                cam[k] = [float(v) if k != "size" else int(v) for v in vals]
+            meta["cameras"][name] = cam
+            out = tmp / "bvh.bin"
+            run("bvh", p, out)
+            b = out.read_bytes()
+            nn, npr = np.frombuffer(b, "<u8", 2)
+            nodes = np.frombuffer(b, crt.NODE_DTYPE, int(nn), 16)
+            order = np.frombuffer(b, "<u4", int(npr), 16 + 64 * int(nn))
+            np.savez_compressed(GOLD / f"bvh_{name}.npz", bounds=nodes["bounds"], index=nodes["index"],
+                                count=nodes["count"], axis=nodes["axis"], order=order)
+        # per-sample-seeded renders
+        for case, name, seed, ov, base, crop in RENDER_CASES:
+            p, d = scene_file(tmp, name, seed, ov)
+            out = tmp / "r.npy"
+            args = ["render", p, base, out] + (list(crop) if crop else [])
+            run(*args)
+            rgb = np.load(out)
+            np.savez_compressed(GOLD / f"render_{case}.npz", rgb=rgb)
+            meta["renders"][case] = {"scene": name, "seed": seed, "camera": ov, "base_seed": base,
+                                     "crop": crop, "shape": list(rgb.shape)}
+        for case, name, seed, ov, base, crop in SAMPLE_CASES:
+            p, d = scene_file(tmp, name, seed, ov)
+            out = tmp / "s.npy"
+            run("samples", p, base, out, *crop)
+            smp = np.load(out)
+            np.savez_compressed(GOLD / f"samples_{case}.npz", samples=smp)
+            meta["renders"][case] = {"scene": name, "seed": seed, "camera": ov, "base_seed": base,
+                                     "crop": crop, "shape": list(smp.shape), "per_sample": True}
+        # closest-hit KATs: random rays from points around the scene toward its contents
+        rng = np.random.default_rng(1234)
+        for name, seed, n in HIT_SCENES:
+            p, d = scene_file(tmp, name, seed, {})
+            cam = crt.resolve_camera(d.camera)
+            o = np.array(cam.origin[:]) + rng.normal(0, 0.5, (n, 3))
+            tgt = np.array(cam.pixel00[:]) + rng.uniform(0, 1, (n, 1)) * np.array(cam.pixel_delta_x[:]) * d.camera.image_w \
+                + rng.uniform(0, 1, (n, 1)) * np.array(cam.pixel_delta_y[:]) * d.camera.image_h
+            rays = np.concatenate([o, tgt - o], axis=1)
+            # a quarter of the rays start on the ground / at scene points and point anywhere
+            k = n // 4
+            rays[:k, 3:] = rng.normal(0, 1, (k, 3))
+            rays_path = tmp / "rays.bin"
+            rays_path.write_bytes(rays.astype("<f8").tobytes())
+            out = tmp / "h.npy"
+            run("hits", p, rays_path, out)
+            np.savez_compressed(GOLD / f"hits_{name}.npz", rays=rays, hits=np.load(out))
+    (GOLD / "golden.json").write_text(json.dumps(meta, indent=1, sort_keys=True))
+    print("golden fixtures written to", GOLD)
+
+
+if __name__ == "__main__":
+    main()
