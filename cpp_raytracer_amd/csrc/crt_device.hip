@@ -58,6 +58,9 @@ struct Work {
     uint32_t row_block, tile_count, tile_index;
     uint32_t tiles_x, tiles_y, tiles;  // 8x8 pixel tiles over (owned rows x width)
     uint32_t chunks, chunk_len;        // sample chunks per pixel
+    // LDS layout of the scene-staging kernels (byte offsets / 16-byte padded sizes)
+    uint32_t lds_nodes, lds_refs, lds_spheres, lds_quads, lds_stack;
+    uint32_t bytes_nodes, bytes_refs, bytes_spheres, bytes_quads;
 };
 
 struct Counters {
@@ -167,20 +170,52 @@ __device__ __forceinline__ bool hit_quad(const DevQuad& q, const double o[3], co
     return false;
 }
 
-// Per-lane traversal stack. LDS: [level][lane] so a wave's pushes hit 64 distinct banks.
-// GLOBAL: the same interleave in an HBM buffer, for trees deeper than the LDS stack.
-template <int SD, bool GLOBAL>
+// Resolve the hit record (hittable.h:46-71): hit point ray(t), outward normal, front face.
+__device__ __forceinline__ uint32_t hit_record(const SceneView& S, uint32_t ref, const double o[3],
+                                               const double d[3], double t, double p[3],
+                                               double nrm[3], bool& front) {
+    p[0] = o[0] + d[0] * t;
+    p[1] = o[1] + d[1] * t;
+    p[2] = o[2] + d[2] * t;
+    double nx, ny, nz;
+    uint32_t m;
+    if (ref & kRefQuad) {
+        const DevQuad& q = S.quads[ref & ~kRefQuad];
+        nx = q.n[0]; ny = q.n[1]; nz = q.n[2];
+        m = S.quad_mat[ref & ~kRefQuad];
+    } else {
+        const DevSphere& sp = S.spheres[ref];
+        const double ir = 1 / sp.r;  // (hit_point - center) / radius
+        nx = (p[0] - sp.c[0]) * ir;
+        ny = (p[1] - sp.c[1]) * ir;
+        nz = (p[2] - sp.c[2]) * ir;
+        m = S.sphere_mat[ref];
+    }
+    if (d[0] * nx + d[1] * ny + d[2] * nz > 0) {
+        nrm[0] = -nx; nrm[1] = -ny; nrm[2] = -nz;
+        front = false;
+    } else {
+        nrm[0] = nx; nrm[1] = ny; nrm[2] = nz;
+        front = true;
+    }
+    return m;
+}
+
+// Per-lane traversal stack, interleaved [level][lane] so a wave's pushes hit distinct banks
+// (LDS) or whole lines (HBM fallback for trees deeper than the LDS budget). Entries are u16 when
+// the BVH has < 65536 nodes.
+template <typename SE>
 struct Stack {
-    uint32_t* base;
+    SE* base;
     uint32_t stride;
-    __device__ __forceinline__ void put(int i, uint32_t v) { base[static_cast<size_t>(i) * stride] = v; }
+    __device__ __forceinline__ void put(int i, uint32_t v) { base[static_cast<size_t>(i) * stride] = static_cast<SE>(v); }
     __device__ __forceinline__ uint32_t get(int i) const { return base[static_cast<size_t>(i) * stride]; }
 };
 
 // BVH::hit_by (bvh.h:585-715): iterative DFS over the preorder nodes, near child first by the
 // sign of the ray direction on the split axis, leaf primitives in order shrinking t_max.
-template <int SD, bool GLOBAL, bool COUNT>
-__device__ __forceinline__ bool trace(const SceneView& S, Stack<SD, GLOBAL>& st, const double o[3],
+template <typename SE, bool COUNT>
+__device__ __forceinline__ bool trace(const SceneView& S, Stack<SE>& st, const double o[3],
                                       const double d[3], double tmin, double& tmax,
                                       uint32_t& hit_ref, Counters& ctr) {
     const double inv[3] = {1 / d[0], 1 / d[1], 1 / d[2]};
@@ -232,197 +267,206 @@ __device__ __forceinline__ bool trace(const SceneView& S, Stack<SD, GLOBAL>& st,
     return found;
 }
 
-// Resolve the hit record (hittable.h:46-71): hit point ray(t), outward normal, front face.
-__device__ __forceinline__ uint32_t hit_record(const SceneView& S, uint32_t ref, const double o[3],
-                                               const double d[3], double t, double p[3],
-                                               double nrm[3], bool& front) {
-    p[0] = o[0] + d[0] * t;
-    p[1] = o[1] + d[1] * t;
-    p[2] = o[2] + d[2] * t;
-    double nx, ny, nz;
-    uint32_t m;
-    if (ref & kRefQuad) {
-        const DevQuad& q = S.quads[ref & ~kRefQuad];
-        nx = q.n[0]; ny = q.n[1]; nz = q.n[2];
-        m = S.quad_mat[ref & ~kRefQuad];
-    } else {
-        const DevSphere& sp = S.spheres[ref];
-        const double ir = 1 / sp.r;  // (hit_point - center) / radius
-        nx = (p[0] - sp.c[0]) * ir;
-        ny = (p[1] - sp.c[1]) * ir;
-        nz = (p[2] - sp.c[2]) * ir;
-        m = S.sphere_mat[ref];
-    }
-    if (d[0] * nx + d[1] * ny + d[2] * nz > 0) {
-        nrm[0] = -nx; nrm[1] = -ny; nrm[2] = -nz;
-        front = false;
-    } else {
-        nrm[0] = nx; nrm[1] = ny; nrm[2] = nz;
-        front = true;
-    }
-    return m;
-}
-
 __device__ __forceinline__ uint32_t owned_row(const Work& w, uint32_t k) {
     uint32_t blk = k / w.row_block, in = k % w.row_block;
     return (blk * w.tile_count + w.tile_index) * w.row_block + in;
 }
 
-// One path (camera.h:184-258) with forward radiance accumulation.
-template <int SD, bool GLOBAL, bool COUNT>
-__device__ __forceinline__ void trace_path(const SceneView& S, const CamView& C, Stack<SD, GLOBAL>& st,
-                                           uint32_t row, uint32_t col, uint32_t rng,
-                                           double L[3], Counters& ctr) {
-    // random_ray_through_pixel (camera.h:184-200)
+// State of one lane's current path: the ray, the throughput, the radiance gathered so far and the
+// bounces left (ray_color's depth_left, camera.h:207-213).
+struct Path {
     double o[3], d[3];
+    double T[3], L[3];
+    uint32_t depth;
+    uint32_t rng;
+};
+
+// random_ray_through_pixel (camera.h:184-200) for a fresh sample
+__device__ __forceinline__ void start_path(const CamView& C, uint32_t row, uint32_t col, uint32_t rng, Path& P) {
     if (C.defocus_angle <= 0) {
-        o[0] = C.o[0]; o[1] = C.o[1]; o[2] = C.o[2];
+        P.o[0] = C.o[0]; P.o[1] = C.o[1]; P.o[2] = C.o[2];
     } else {  // random_point_in_defocus_disk (camera.h:160-168, vec3d.h:79-85)
         double vx, vy;
         do {
             vx = rnd(rng, -1, 1);
             vy = rnd(rng, -1, 1);
         } while (!(vx * vx + vy * vy + 0.0 * 0.0 < 1));
-        o[0] = (C.o[0] + C.ddx[0] * vx) + C.ddy[0] * vy;
-        o[1] = (C.o[1] + C.ddx[1] * vx) + C.ddy[1] * vy;
-        o[2] = (C.o[2] + C.ddx[2] * vx) + C.ddy[2] * vy;
+        P.o[0] = (C.o[0] + C.ddx[0] * vx) + C.ddy[0] * vy;
+        P.o[1] = (C.o[1] + C.ddx[1] * vx) + C.ddy[1] * vy;
+        P.o[2] = (C.o[2] + C.ddx[2] * vx) + C.ddy[2] * vy;
     }
     const double fr = static_cast<double>(row), fc = static_cast<double>(col);
     // a g++ build evaluates the second jitter draw (the pixel_delta_y one) first
     const double uy = rnd(rng, -0.5, 0.5);
     const double ux = rnd(rng, -0.5, 0.5);
+#pragma unroll
     for (int k = 0; k < 3; ++k) {
-        double center = (C.p00[k] + C.pdy[k] * fr) + C.pdx[k] * fc;
-        double sample = (center + C.pdx[k] * ux) + C.pdy[k] * uy;
-        d[k] = sample - o[k];
+        const double center = (C.p00[k] + C.pdy[k] * fr) + C.pdx[k] * fc;
+        const double sample = (center + C.pdx[k] * ux) + C.pdy[k] * uy;
+        P.d[k] = sample - P.o[k];
+        P.T[k] = 1;
+        P.L[k] = 0;
     }
-    double T[3] = {1, 1, 1};
-    L[0] = L[1] = L[2] = 0;
-    for (uint32_t depth = C.max_depth; depth > 0; --depth) {
-        if (COUNT) ctr.rays++;
-        double tmax = __builtin_inf();
-        uint32_t ref = 0;
-        if (!trace<SD, GLOBAL, COUNT>(S, st, o, d, C.t_min, tmax, ref, ctr)) {
-            L[0] += T[0] * C.bg[0];
-            L[1] += T[1] * C.bg[1];
-            L[2] += T[2] * C.bg[2];
-            return;
-        }
-        double p[3], n[3];
-        bool front;
-        const uint32_t mi = hit_record(S, ref, o, d, tmax, p, n, front);
-        const DevMaterial& M = S.mats[mi];
-        double nd[3];
-        if (M.kind == CRT_LAMBERTIAN) {  // material.h:64-86
-            double rx, ry, rz;
-            random_unit_vector(rng, rx, ry, rz);
-            nd[0] = n[0] + rx; nd[1] = n[1] + ry; nd[2] = n[2] + rz;
-            if (fabs(nd[0]) < 1e-8 && fabs(nd[1]) < 1e-8 && fabs(nd[2]) < 1e-8) {
-                nd[0] = n[0]; nd[1] = n[1]; nd[2] = n[2];
-            }
-        } else if (M.kind == CRT_METAL) {  // material.h:116-139
-            const double il = 1 / sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
-            const double ux0 = d[0] * il, uy0 = d[1] * il, uz0 = d[2] * il;
-            const double k2 = 2 * (ux0 * n[0] + uy0 * n[1] + uz0 * n[2]);
-            double rx, ry, rz;
-            random_unit_vector(rng, rx, ry, rz);
-            nd[0] = (ux0 - n[0] * k2) + rx * M.param;
-            nd[1] = (uy0 - n[1] * k2) + ry * M.param;
-            nd[2] = (uz0 - n[2] * k2) + rz * M.param;
-            if (n[0] * nd[0] + n[1] * nd[1] + n[2] * nd[2] < 0) return;  // absorbed; emits 0
-        } else if (M.kind == CRT_DIELECTRIC) {  // material.h:185-218, vec3d.h:144-200
-            const double ratio = front ? 1. / M.param : M.param / 1.;
-            const double il = 1 / sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
-            const double ux0 = d[0] * il, uy0 = d[1] * il, uz0 = d[2] * il;
-            const double cosv = fmin((-ux0) * n[0] + (-uy0) * n[1] + (-uz0) * n[2], 1.);
-            const double sinv = sqrt(1 - cosv * cosv);
-            bool reflect;
-            if (ratio * sinv > 1) {
-                reflect = true;  // total internal reflection, no draw
-            } else {
-                double r0 = (1 - ratio) / (1 + ratio);
-                r0 = r0 * r0;
-                const double refl = r0 + (1 - r0) * pow5(1 - cosv);
-                reflect = rnd(rng, 0, 1) < refl;
-            }
-            if (reflect) {
-                const double k2 = 2 * (ux0 * n[0] + uy0 * n[1] + uz0 * n[2]);
-                nd[0] = ux0 - n[0] * k2;
-                nd[1] = uy0 - n[1] * k2;
-                nd[2] = uz0 - n[2] * k2;
-            } else {
-                const double px = (ux0 + n[0] * cosv) * ratio;
-                const double py = (uy0 + n[1] * cosv) * ratio;
-                const double pz = (uz0 + n[2] * cosv) * ratio;
-                const double s = -sqrt(fabs(1 - (px * px + py * py + pz * pz)));
-                nd[0] = px + n[0] * s;
-                nd[1] = py + n[1] * s;
-                nd[2] = pz + n[2] * s;
-            }
-        } else {  // DiffuseLight: emits, never scatters (material.h:248-263)
-            L[0] += T[0] * M.emit[0];
-            L[1] += T[1] * M.emit[1];
-            L[2] += T[2] * M.emit[2];
-            return;
-        }
-        if (M.kind != CRT_DIELECTRIC) {  // attenuation = intrinsic colour (dielectric: 1)
-            T[0] = T[0] * M.color[0];
-            T[1] = T[1] * M.color[1];
-            T[2] = T[2] * M.color[2];
-        }
-        o[0] = p[0]; o[1] = p[1]; o[2] = p[2];
-        d[0] = nd[0]; d[1] = nd[1]; d[2] = nd[2];
-    }
-    // depth exhausted: ray_color returns RGB::zero() (camera.h:211-213)
+    P.depth = C.max_depth;
+    P.rng = rng;
 }
 
-// The render kernel. Thread -> (sample chunk, pixel); each wave owns one 8x8 pixel tile so
-// primary rays of a wave are coherent. Each thread sums its chunk's samples in sample order into
-// partial[chunk][pixel].
-template <int SD, bool GLOBAL, bool COUNT>
-__global__ __launch_bounds__(kBlock) void render_kernel(SceneView S, CamView C, Work W,
+// One level of ray_color (camera.h:205-258) after the closest-hit query: gathers emission or
+// background into L, scatters (material.h:64-263) into the next ray. Returns true when the path
+// has ended (miss, light, absorption).
+__device__ __forceinline__ bool shade(const SceneView& S, const CamView& C, Path& P, bool hit,
+                                      uint32_t ref, double t) {
+    if (!hit) {
+        P.L[0] += P.T[0] * C.bg[0];
+        P.L[1] += P.T[1] * C.bg[1];
+        P.L[2] += P.T[2] * C.bg[2];
+        return true;
+    }
+    double p[3], n[3];
+    bool front;
+    const uint32_t mi = hit_record(S, ref, P.o, P.d, t, p, n, front);
+    const DevMaterial& M = S.mats[mi];
+    const uint32_t kind = M.kind;
+    double nd[3];
+    if (kind == CRT_LAMBERTIAN) {  // material.h:64-86
+        double rx, ry, rz;
+        random_unit_vector(P.rng, rx, ry, rz);
+        nd[0] = n[0] + rx; nd[1] = n[1] + ry; nd[2] = n[2] + rz;
+        if (fabs(nd[0]) < 1e-8 && fabs(nd[1]) < 1e-8 && fabs(nd[2]) < 1e-8) {
+            nd[0] = n[0]; nd[1] = n[1]; nd[2] = n[2];
+        }
+    } else if (kind == CRT_METAL) {  // material.h:116-139
+        const double il = 1 / sqrt(P.d[0] * P.d[0] + P.d[1] * P.d[1] + P.d[2] * P.d[2]);
+        const double ux0 = P.d[0] * il, uy0 = P.d[1] * il, uz0 = P.d[2] * il;
+        const double k2 = 2 * (ux0 * n[0] + uy0 * n[1] + uz0 * n[2]);
+        double rx, ry, rz;
+        random_unit_vector(P.rng, rx, ry, rz);
+        nd[0] = (ux0 - n[0] * k2) + rx * M.param;
+        nd[1] = (uy0 - n[1] * k2) + ry * M.param;
+        nd[2] = (uz0 - n[2] * k2) + rz * M.param;
+        if (n[0] * nd[0] + n[1] * nd[1] + n[2] * nd[2] < 0) return true;  // absorbed; emits 0
+    } else if (kind == CRT_DIELECTRIC) {  // material.h:185-218, vec3d.h:144-200
+        const double ratio = front ? 1. / M.param : M.param / 1.;
+        const double il = 1 / sqrt(P.d[0] * P.d[0] + P.d[1] * P.d[1] + P.d[2] * P.d[2]);
+        const double ux0 = P.d[0] * il, uy0 = P.d[1] * il, uz0 = P.d[2] * il;
+        const double cosv = fmin((-ux0) * n[0] + (-uy0) * n[1] + (-uz0) * n[2], 1.);
+        const double sinv = sqrt(1 - cosv * cosv);
+        bool reflect;
+        if (ratio * sinv > 1) {
+            reflect = true;  // total internal reflection, no draw
+        } else {
+            double r0 = (1 - ratio) / (1 + ratio);
+            r0 = r0 * r0;
+            const double refl = r0 + (1 - r0) * pow5(1 - cosv);
+            reflect = rnd(P.rng, 0, 1) < refl;
+        }
+        if (reflect) {
+            const double k2 = 2 * (ux0 * n[0] + uy0 * n[1] + uz0 * n[2]);
+            nd[0] = ux0 - n[0] * k2;
+            nd[1] = uy0 - n[1] * k2;
+            nd[2] = uz0 - n[2] * k2;
+        } else {
+            const double px = (ux0 + n[0] * cosv) * ratio;
+            const double py = (uy0 + n[1] * cosv) * ratio;
+            const double pz = (uz0 + n[2] * cosv) * ratio;
+            const double s = -sqrt(fabs(1 - (px * px + py * py + pz * pz)));
+            nd[0] = px + n[0] * s;
+            nd[1] = py + n[1] * s;
+            nd[2] = pz + n[2] * s;
+        }
+    } else {  // DiffuseLight: emits, never scatters (material.h:248-263)
+        P.L[0] += P.T[0] * M.emit[0];
+        P.L[1] += P.T[1] * M.emit[1];
+        P.L[2] += P.T[2] * M.emit[2];
+        return true;
+    }
+    if (kind != CRT_DIELECTRIC) {  // attenuation = intrinsic colour (dielectric: 1)
+        P.T[0] = P.T[0] * M.color[0];
+        P.T[1] = P.T[1] * M.color[1];
+        P.T[2] = P.T[2] * M.color[2];
+    }
+    P.o[0] = p[0]; P.o[1] = p[1]; P.o[2] = p[2];
+    P.d[0] = nd[0]; P.d[1] = nd[1]; P.d[2] = nd[2];
+    P.depth -= 1;
+    return false;
+}
+
+// 16-byte cooperative copy global -> LDS (the scene staging of LSCENE kernels)
+__device__ __forceinline__ void stage_lds(unsigned char* dst, const void* src, uint32_t bytes) {
+    const uint4* s = static_cast<const uint4*>(src);
+    uint4* d = reinterpret_cast<uint4*>(dst);
+    for (uint32_t i = threadIdx.x; i < bytes / 16; i += kBlock) d[i] = s[i];
+}
+
+// The render kernel. Thread -> (sample chunk, pixel); each wave starts on one 8x8 pixel tile.
+// A lane loops over its chunk's samples with path regeneration: one iteration = one ray segment
+// (closest hit + shade); when a path ends the lane starts its next sample at once, so a wave is
+// never held by its longest path. Samples are summed in sample order into partial[chunk][pixel].
+// LSCENE: nodes, primitive refs, spheres and parallelograms are staged in LDS first.
+template <typename SE, bool GSTACK, bool LSCENE, bool COUNT>
+__global__ __launch_bounds__(kBlock) void render_kernel(SceneView Sg, CamView C, Work W,
                                                         double* __restrict__ partial,
-                                                        uint32_t* __restrict__ gstack,
+                                                        SE* __restrict__ gstack,
                                                         Counters* __restrict__ counters) {
-    __shared__ uint32_t lstack[GLOBAL ? 1 : SD * kBlock];
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    SceneView S = Sg;
+    if (LSCENE) {
+        stage_lds(smem + W.lds_nodes, Sg.nodes, W.bytes_nodes);
+        stage_lds(smem + W.lds_refs, Sg.refs, W.bytes_refs);
+        stage_lds(smem + W.lds_spheres, Sg.spheres, W.bytes_spheres);
+        stage_lds(smem + W.lds_quads, Sg.quads, W.bytes_quads);
+        S.nodes = reinterpret_cast<const DevNode*>(smem + W.lds_nodes);
+        S.refs = reinterpret_cast<const uint32_t*>(smem + W.lds_refs);
+        S.spheres = reinterpret_cast<const DevSphere*>(smem + W.lds_spheres);
+        S.quads = reinterpret_cast<const DevQuad*>(smem + W.lds_quads);
+        __syncthreads();
+    }
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t wave = (static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x) >> 6;
     const uint32_t chunk = static_cast<uint32_t>(wave / W.tiles);
     const uint32_t tile = static_cast<uint32_t>(wave % W.tiles);
     Counters ctr{0, 0, 0, 0};
-    if (chunk < W.chunks) {
-        const uint32_t tx = tile % W.tiles_x, ty = tile / W.tiles_x;
-        const uint32_t col = tx * 8 + (lane & 7);
-        const uint32_t k = ty * 8 + (lane >> 3);
-        if (col < C.w && k < W.owned_rows) {
-            const uint32_t row = owned_row(W, k);
-            Stack<SD, GLOBAL> st;
-            if (GLOBAL) {
-                const uint32_t stride = gridDim.x * kBlock;
-                st.base = gstack + (static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x);
-                st.stride = stride;
-            } else {
-                st.base = lstack + threadIdx.x;
-                st.stride = kBlock;
+    const uint32_t tx = tile % W.tiles_x, ty = tile / W.tiles_x;
+    const uint32_t col = tx * 8 + (lane & 7);
+    const uint32_t k = ty * 8 + (lane >> 3);
+    if (chunk < W.chunks && col < C.w && k < W.owned_rows) {
+        const uint32_t row = owned_row(W, k);
+        Stack<SE> st;
+        if (GSTACK) {
+            st.base = gstack + (static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x);
+            st.stride = gridDim.x * kBlock;
+        } else {
+            st.base = reinterpret_cast<SE*>(smem + W.lds_stack) + threadIdx.x;
+            st.stride = kBlock;
+        }
+        const uint32_t pixel = row * C.w + col;
+        uint32_t s = chunk * W.chunk_len;
+        const uint32_t s_end = min(C.spp, s + W.chunk_len);
+        double acc[3] = {0, 0, 0};
+        Path P;
+        start_path(C, row, col, sample_seed(C.base_seed, pixel, s), P);
+        while (true) {
+            bool ended = true;
+            if (P.depth > 0) {
+                if (COUNT) ctr.rays++;
+                double tmax = __builtin_inf();
+                uint32_t ref = 0;
+                const bool hit = trace<SE, COUNT>(S, st, P.o, P.d, C.t_min, tmax, ref, ctr);
+                ended = shade(S, C, P, hit, ref, tmax);
+            }  // depth exhausted: ray_color returns RGB::zero() (camera.h:211-213)
+            if (ended) {
+                acc[0] = acc[0] + P.L[0];
+                acc[1] = acc[1] + P.L[1];
+                acc[2] = acc[2] + P.L[2];
+                if (++s >= s_end) break;
+                start_path(C, row, col, sample_seed(C.base_seed, pixel, s), P);
             }
-            const uint32_t pixel = row * C.w + col;
-            const uint32_t s0 = chunk * W.chunk_len;
-            const uint32_t s1 = min(C.spp, s0 + W.chunk_len);
-            double acc[3] = {0, 0, 0};
-            for (uint32_t s = s0; s < s1; ++s) {
-                double L[3];
-                trace_path<SD, GLOBAL, COUNT>(S, C, st, row, col, sample_seed(C.base_seed, pixel, s),
-                                              L, ctr);
-                acc[0] = acc[0] + L[0];
-                acc[1] = acc[1] + L[1];
-                acc[2] = acc[2] + L[2];
-            }
-            if (!COUNT) {
-                double* dst = partial + (static_cast<size_t>(chunk) * C.h * C.w + pixel) * 3;
-                dst[0] = acc[0];
-                dst[1] = acc[1];
-                dst[2] = acc[2];
-            }
+        }
+        if (!COUNT) {
+            double* dst = partial + (static_cast<size_t>(chunk) * C.h * C.w + pixel) * 3;
+            dst[0] = acc[0];
+            dst[1] = acc[1];
+            dst[2] = acc[2];
         }
     }
     if (COUNT) {
@@ -463,7 +507,7 @@ __global__ __launch_bounds__(kBlock) void hits_kernel(SceneView S, const double*
                                                       uint32_t* __restrict__ gstack) {
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
-    Stack<0, true> st;
+    Stack<uint32_t> st;
     st.base = gstack + i;
     st.stride = gridDim.x * kBlock;
     double o[3] = {rays[6 * i + 0], rays[6 * i + 1], rays[6 * i + 2]};
@@ -473,7 +517,7 @@ __global__ __launch_bounds__(kBlock) void hits_kernel(SceneView S, const double*
     Counters ctr{};
     crt_hit h{};
     h.prim = -1;
-    if (trace<0, true, false>(S, st, o, d, t_min, tmax, ref, ctr)) {
+    if (trace<uint32_t, false>(S, st, o, d, t_min, tmax, ref, ctr)) {
         double p[3], nrm[3];
         bool front;
         h.material = hit_record(S, ref, o, d, tmax, p, nrm, front);
@@ -613,31 +657,35 @@ static uint32_t count_owned(uint32_t h, uint32_t rb, uint32_t tc, uint32_t ti) {
     return n;
 }
 
-// resident threads of the render kernel on this device (for the sample-chunk split)
-template <int SD, bool GLOBAL>
-static size_t resident_threads(int device) {
-    static size_t cached[kMaxDevices] = {};
-    if (cached[device]) return cached[device];
+static size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
+
+constexpr size_t kLdsSceneBudget = 40 * 1024;  // scene + stack; keeps >= 3 blocks (12 waves)/CU
+constexpr size_t kLdsStackBudget = 32 * 1024;
+
+template <typename SE, bool GSTACK, bool LSCENE, bool COUNT>
+static const void* kernel_ptr() {
+    return reinterpret_cast<const void*>(dev::render_kernel<SE, GSTACK, LSCENE, COUNT>);
+}
+
+// resident threads of a render-kernel variant on this device (for the sample-chunk split)
+static size_t resident_threads(const void* fn, size_t lds, int device) {
     int blocks = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &blocks, reinterpret_cast<const void*>(dev::render_kernel<SD, GLOBAL, false>),
-            dev::kBlock, 0) != hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fn, dev::kBlock, lds) != hipSuccess ||
         blocks <= 0)
         blocks = 2;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
         cus = 256;
-    cached[device] = static_cast<size_t>(blocks) * cus * dev::kBlock;
-    return cached[device];
+    return static_cast<size_t>(blocks) * cus * dev::kBlock;
 }
 
-template <int SD, bool GLOBAL>
+template <typename SE, bool GSTACK, bool LSCENE>
 static int launch_render(const crt_scene* s, int device, const crt_camera* cam, const dev::Work& w0,
-                         double* d_rgb, hipStream_t stream, crt_render_stats* count_stats) {
+                         size_t lds, double* d_rgb, hipStream_t stream, crt_render_stats* count_stats) {
     const DeviceCopy& c = s->dev[device];
     dev::Work W = w0;
     const uint64_t pixels = static_cast<uint64_t>(W.owned_rows) * cam->image_w;
-    const size_t resident = resident_threads<SD, GLOBAL>(device);
-    // enough threads for ~8 waves of residency so block-level dynamic dispatch balances rows of
+    const size_t resident = resident_threads(kernel_ptr<SE, GSTACK, LSCENE, false>(), lds, device);
+    // enough threads for ~8 rounds of residency so block-level dynamic dispatch balances rows of
     // very different cost; never split below 1 sample per thread
     uint64_t want = (8 * static_cast<uint64_t>(resident) + pixels - 1) / std::max<uint64_t>(1, pixels);
     W.chunks = static_cast<uint32_t>(std::min<uint64_t>(std::max<uint64_t>(1, want), cam->samples_per_pixel));
@@ -649,12 +697,13 @@ static int launch_render(const crt_scene* s, int device, const crt_camera* cam, 
     const size_t plane = static_cast<size_t>(cam->image_h) * cam->image_w * 3;
 
     double* partial = nullptr;
-    uint32_t* gstack = nullptr;
+    SE* gstack = nullptr;
     dev::Counters* ctr = nullptr;
     const bool count = count_stats != nullptr;
-    if (!count) HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&partial), plane * W.chunks * sizeof(double), stream));
-    if (GLOBAL) {
-        size_t bytes = static_cast<size_t>(s->depth + 1) * blocks * dev::kBlock * 4;
+    if (!count)
+        HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&partial), plane * W.chunks * sizeof(double), stream));
+    if (GSTACK) {
+        size_t bytes = static_cast<size_t>(s->depth + 1) * blocks * dev::kBlock * sizeof(SE);
         HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&gstack), bytes, stream));
     }
     if (count) {
@@ -668,16 +717,15 @@ static int launch_render(const crt_scene* s, int device, const crt_camera* cam, 
         HIP_TRY(hipEventCreate(&e0));
         HIP_TRY(hipEventCreate(&e1));
         HIP_TRY(hipEventRecord(e0, stream));
-        hipLaunchKernelGGL((dev::render_kernel<SD, GLOBAL, true>), dim3(static_cast<uint32_t>(blocks)),
-                           dim3(dev::kBlock), 0, stream, S, C, W, partial, gstack, ctr);
+        hipLaunchKernelGGL((dev::render_kernel<SE, GSTACK, LSCENE, true>), dim3(static_cast<uint32_t>(blocks)),
+                           dim3(dev::kBlock), lds, stream, S, C, W, partial, gstack, ctr);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(e1, stream));
     } else {
-        hipLaunchKernelGGL((dev::render_kernel<SD, GLOBAL, false>), dim3(static_cast<uint32_t>(blocks)),
-                           dim3(dev::kBlock), 0, stream, S, C, W, partial, gstack, ctr);
+        hipLaunchKernelGGL((dev::render_kernel<SE, GSTACK, LSCENE, false>), dim3(static_cast<uint32_t>(blocks)),
+                           dim3(dev::kBlock), lds, stream, S, C, W, partial, gstack, ctr);
         HIP_TRY(hipGetLastError());
-        const uint64_t n = pixels;
-        const uint32_t rb = static_cast<uint32_t>((n + 255) / 256);
+        const uint32_t rb = static_cast<uint32_t>((pixels + 255) / 256);
         if (rb) {
             hipLaunchKernelGGL(dev::resolve_kernel, dim3(rb), dim3(256), 0, stream, partial, d_rgb,
                                W, cam->image_w, cam->image_h, C.inv_spp);
@@ -691,6 +739,7 @@ static int launch_render(const crt_scene* s, int device, const crt_camera* cam, 
         HIP_TRY(hipMemcpyAsync(&h, ctr, sizeof h, hipMemcpyDeviceToHost, stream));
         HIP_TRY(hipStreamSynchronize(stream));
         HIP_TRY(hipFreeAsync(ctr, stream));
+        HIP_TRY(hipStreamSynchronize(stream));
         float ms = 0;
         HIP_TRY(hipEventElapsedTime(&ms, e0, e1));
         (void)hipEventDestroy(e0);
@@ -703,6 +752,33 @@ static int launch_render(const crt_scene* s, int device, const crt_camera* cam, 
         count_stats->kernel_ms = ms;
     }
     return CRT_OK;
+}
+
+// Kernel variant per scene: u16 stack entries below 65536 nodes; the scene itself in LDS when it
+// and the stack fit the LDS budget, else the stack alone in LDS, else everything in HBM.
+template <typename SE>
+static int dispatch_render(const crt_scene* s, int device, const crt_camera* cam, dev::Work W,
+                           double* d_rgb, hipStream_t st, crt_render_stats* count_stats) {
+    const size_t stack_bytes = align16(static_cast<size_t>(std::max<uint32_t>(1, s->depth)) * dev::kBlock * sizeof(SE));
+    W.bytes_nodes = static_cast<uint32_t>(align16(s->dnodes.size() * sizeof(DevNode)));
+    W.bytes_refs = static_cast<uint32_t>(align16(s->refs.size() * 4));
+    W.bytes_spheres = static_cast<uint32_t>(align16(s->spheres.size() * sizeof(DevSphere)));
+    W.bytes_quads = static_cast<uint32_t>(align16(s->quads.size() * sizeof(DevQuad)));
+    const size_t scene_bytes = static_cast<size_t>(W.bytes_nodes) + W.bytes_refs + W.bytes_spheres + W.bytes_quads;
+    const bool force_global = std::getenv("CRT_NO_LDS_SCENE") != nullptr;
+    if (!force_global && scene_bytes + stack_bytes <= kLdsSceneBudget) {
+        W.lds_nodes = 0;
+        W.lds_refs = W.lds_nodes + W.bytes_nodes;
+        W.lds_spheres = W.lds_refs + W.bytes_refs;
+        W.lds_quads = W.lds_spheres + W.bytes_spheres;
+        W.lds_stack = W.lds_quads + W.bytes_quads;
+        return launch_render<SE, false, true>(s, device, cam, W, scene_bytes + stack_bytes, d_rgb, st, count_stats);
+    }
+    if (stack_bytes <= kLdsStackBudget) {
+        W.lds_stack = 0;
+        return launch_render<SE, false, false>(s, device, cam, W, stack_bytes, d_rgb, st, count_stats);
+    }
+    return launch_render<SE, true, false>(s, device, cam, W, 0, d_rgb, st, count_stats);
 }
 
 int device_render(const crt_scene* s, int device, const crt_camera* cam, const crt_tiling* t,
@@ -747,13 +823,10 @@ int device_render(const crt_scene* s, int device, const crt_camera* cam, const c
     hipStream_t st = static_cast<hipStream_t>(stream);
     if (count_stats) HIP_TRY(hipStreamCreate(&st));
     int r;
-    // stack entries needed <= depth - 1
-    if (s->depth <= 17)
-        r = launch_render<16, false>(s, device, cam, W, d_rgb, st, count_stats);
-    else if (s->depth <= 33)
-        r = launch_render<32, false>(s, device, cam, W, d_rgb, st, count_stats);
+    if (s->dnodes.size() < 65536)
+        r = dispatch_render<uint16_t>(s, device, cam, W, d_rgb, st, count_stats);
     else
-        r = launch_render<0, true>(s, device, cam, W, d_rgb, st, count_stats);
+        r = dispatch_render<uint32_t>(s, device, cam, W, d_rgb, st, count_stats);
     if (count_stats) (void)hipStreamDestroy(st);
     return r;
 }
