@@ -214,6 +214,10 @@ struct Stack {
 
 // BVH::hit_by (bvh.h:585-715): iterative DFS over the preorder nodes, near child first by the
 // sign of the ray direction on the split axis, leaf primitives in order shrinking t_max.
+// Control flow is "while-while" (Aila & Laine 2009): a lane walks interior nodes until it enters
+// a leaf (or finishes), and the wave then tests all lanes' leaves together, so the primitive loop
+// runs with most lanes active. Per lane, the sequence of node tests and primitive tests is
+// exactly the reference's.
 template <typename SE, bool COUNT>
 __device__ __forceinline__ bool trace(const SceneView& S, Stack<SE>& st, const double o[3],
                                       const double d[3], double tmin, double& tmax,
@@ -224,33 +228,19 @@ __device__ __forceinline__ bool trace(const SceneView& S, Stack<SE>& st, const d
     bool found = false;
     int sp = 0;
     uint32_t cur = 0;
-    while (true) {
-        const DevNode& n = S.nodes[cur];
-        if (COUNT) ctr.nodes++;
-        const bool enter = (n.flags & kNodeAlways) || slab(n, o, inv, neg, tmin, tmax);
-        if (enter) {
-            if (n.count > 0) {
-                const uint32_t end = n.index + n.count;
-                for (uint32_t i = n.index; i < end; ++i) {
-                    const uint32_t ref = S.refs[i];
-                    double t;
-                    bool h;
-                    if (ref & kRefQuad) {
-                        if (COUNT) ctr.quad_tests++;
-                        h = hit_quad(S.quads[ref & ~kRefQuad], o, d, tmin, tmax, t);
-                    } else {
-                        if (COUNT) ctr.sphere_tests++;
-                        h = hit_sphere(S.spheres[ref], o, d, a, tmin, tmax, t);
-                    }
-                    if (h) {
-                        tmax = t;
-                        hit_ref = ref;
-                        found = true;
-                    }
+    bool done = false;
+    while (!done) {
+        uint32_t first = 0, count = 0;
+        while (true) {  // interior walk until a leaf is entered
+            const DevNode& n = S.nodes[cur];
+            if (COUNT) ctr.nodes++;
+            const bool enter = (n.flags & kNodeAlways) || slab(n, o, inv, neg, tmin, tmax);
+            if (enter) {
+                if (n.count > 0) {
+                    first = n.index;
+                    count = n.count;
+                    break;
                 }
-                if (sp == 0) break;
-                cur = st.get(--sp);
-            } else {
                 if (neg[n.axis]) {
                     st.put(sp++, cur + 1);
                     cur = n.index;
@@ -258,10 +248,34 @@ __device__ __forceinline__ bool trace(const SceneView& S, Stack<SE>& st, const d
                     st.put(sp++, n.index);
                     cur = cur + 1;
                 }
+            } else {
+                if (sp == 0) {
+                    done = true;
+                    break;
+                }
+                cur = st.get(--sp);
             }
-        } else {
-            if (sp == 0) break;
-            cur = st.get(--sp);
+        }
+        for (uint32_t i = first; i < first + count; ++i) {  // the entered leaf's primitives
+            const uint32_t ref = S.refs[i];
+            double t;
+            bool h;
+            if (ref & kRefQuad) {
+                if (COUNT) ctr.quad_tests++;
+                h = hit_quad(S.quads[ref & ~kRefQuad], o, d, tmin, tmax, t);
+            } else {
+                if (COUNT) ctr.sphere_tests++;
+                h = hit_sphere(S.spheres[ref], o, d, a, tmin, tmax, t);
+            }
+            if (h) {
+                tmax = t;
+                hit_ref = ref;
+                found = true;
+            }
+        }
+        if (count > 0) {
+            if (sp == 0) done = true;
+            else cur = st.get(--sp);
         }
     }
     return found;
