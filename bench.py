@@ -216,6 +216,8 @@ def main():
                      "peak_tflops": FP64_VECTOR_PEAK_TFLOPS, "rays_per_sample": round(rays_per_sample, 4),
                      "nodes_per_ray": round(cnt.nodes_visited / max(1, cnt.rays), 3),
                      "prim_tests_per_ray": round((cnt.sphere_tests + cnt.parallelogram_tests) / max(1, cnt.rays), 3)},
+            "wave_time_share": {k: round(getattr(cnt, "ticks_" + k) / max(1, cnt.ticks_total), 4)
+                                for k in ("walk", "leaf", "shade")},
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

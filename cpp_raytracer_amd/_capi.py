@@ -12,7 +12,8 @@ from pathlib import Path
 import numpy as np
 
 PKG_DIR = Path(__file__).resolve().parent
-LIB_PATH = PKG_DIR / "lib" / "libcrt_hip.so"
+# CRT_LIB selects an alternative in-tree build (benchmarking variants); default is the product.
+LIB_PATH = Path(os.environ.get("CRT_LIB", PKG_DIR / "lib" / "libcrt_hip.so"))
 
 CRT_LAMBERTIAN, CRT_METAL, CRT_DIELECTRIC, CRT_DIFFUSE_LIGHT = 1, 2, 3, 4
 CRT_SPHERE, CRT_PARALLELOGRAM, CRT_BOX = 1, 2, 3
@@ -78,7 +79,8 @@ class Hit(C.Structure):
 class RenderStats(C.Structure):
     _fields_ = [("samples", C.c_uint64), ("rays", C.c_uint64), ("nodes_visited", C.c_uint64),
                 ("sphere_tests", C.c_uint64), ("parallelogram_tests", C.c_uint64),
-                ("kernel_ms", C.c_double)]
+                ("kernel_ms", C.c_double), ("ticks_walk", C.c_uint64), ("ticks_leaf", C.c_uint64),
+                ("ticks_shade", C.c_uint64), ("ticks_total", C.c_uint64)]
 
 
 # numpy views of the same records (for bulk scene I/O)

@@ -61,10 +61,12 @@ struct Work {
     // LDS layout of the scene-staging kernels (byte offsets / 16-byte padded sizes)
     uint32_t lds_nodes, lds_refs, lds_spheres, lds_quads, lds_stack;
     uint32_t bytes_nodes, bytes_refs, bytes_spheres, bytes_quads;
+    uint32_t sphere_only;   // every primitive is a sphere: refs[slot] == slot
 };
 
 struct Counters {
     unsigned long long rays, nodes, sphere_tests, quad_tests;
+    unsigned long long cyc_walk, cyc_leaf, cyc_shade, cyc_total;  // wave cycles (instrumented pass)
 };
 
 // ---- reference RNG (rand_util.h:85-117) with per-sample state ------------------------------
@@ -108,25 +110,57 @@ __device__ __forceinline__ double pow5(double x) {
     return x5h + x5l;
 }
 
-// AABB::is_hit_by_optimized (aabb.h:132-174)
-__device__ __forceinline__ bool slab(const DevNode& n, const double o[3], const double inv[3],
-                                     const int neg[3], double tmin, double tmax) {
-    double xtmin = (n.b[0 + neg[0]] - o[0]) * inv[0];
-    double xtmax = (n.b[1 - neg[0]] - o[0]) * inv[0];
-    double ytmin = (n.b[2 + neg[1]] - o[1]) * inv[1];
-    double ytmax = (n.b[3 - neg[1]] - o[1]) * inv[1];
-    if (xtmin > ytmax || ytmin > xtmax) return false;
-    if (ytmin > xtmin) xtmin = ytmin;
-    if (ytmax < xtmax) xtmax = ytmax;
-    double ztmin = (n.b[4 + neg[2]] - o[2]) * inv[2];
-    double ztmax = (n.b[5 - neg[2]] - o[2]) * inv[2];
-    if (xtmin > ztmax || ztmin > xtmax) return false;
-    if (ztmin > xtmin) xtmin = ztmin;
-    if (ztmax < xtmax) xtmax = ztmax;
-    return (xtmin < tmax) && (xtmax > tmin);
+// AABB::is_hit_by_optimized (aabb.h:132-174). The early returns of the reference are folded into
+// one boolean (the tests have no side effects), so the whole node is loaded up front (four
+// 16-byte loads) and the test runs without branches.
+struct NodeRegs {
+    double b[6];
+    uint32_t index, count, axis, flags;
+};
+
+__device__ __forceinline__ NodeRegs load_node(const DevNode* nodes, uint32_t i) {
+    const uint4* p = reinterpret_cast<const uint4*>(nodes + i);
+    const uint4 q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3];
+    NodeRegs n;
+    n.b[0] = __hiloint2double(q0.y, q0.x);
+    n.b[1] = __hiloint2double(q0.w, q0.z);
+    n.b[2] = __hiloint2double(q1.y, q1.x);
+    n.b[3] = __hiloint2double(q1.w, q1.z);
+    n.b[4] = __hiloint2double(q2.y, q2.x);
+    n.b[5] = __hiloint2double(q2.w, q2.z);
+    n.index = q3.x;
+    n.count = q3.y;
+    n.axis = q3.z;
+    n.flags = q3.w;
+    return n;
 }
 
-// Sphere::hit_by (sphere.h:45-96) returning the accepted root through t
+__device__ __forceinline__ bool slab(const NodeRegs& n, const double o[3], const double inv[3],
+                                     uint32_t neg, double tmin, double tmax) {
+    // x[neg] / x[!neg]: neg bit k selects max as the entry bound on axis k
+    const double bx0 = (neg & 1u) ? n.b[1] : n.b[0], bx1 = (neg & 1u) ? n.b[0] : n.b[1];
+    const double by0 = (neg & 2u) ? n.b[3] : n.b[2], by1 = (neg & 2u) ? n.b[2] : n.b[3];
+    const double bz0 = (neg & 4u) ? n.b[5] : n.b[4], bz1 = (neg & 4u) ? n.b[4] : n.b[5];
+    double xtmin = (bx0 - o[0]) * inv[0];
+    double xtmax = (bx1 - o[0]) * inv[0];
+    const double ytmin = (by0 - o[1]) * inv[1];
+    const double ytmax = (by1 - o[1]) * inv[1];
+    const double ztmin = (bz0 - o[2]) * inv[2];
+    const double ztmax = (bz1 - o[2]) * inv[2];
+    const bool c1 = !(xtmin > ytmax || ytmin > xtmax);
+    if (ytmin > xtmin) xtmin = ytmin;
+    if (ytmax < xtmax) xtmax = ytmax;
+    const bool c2 = !(xtmin > ztmax || ztmin > xtmax);
+    if (ztmin > xtmin) xtmin = ztmin;
+    if (ztmax < xtmax) xtmax = ztmax;
+    return c1 & c2 & (xtmin < tmax) & (xtmax > tmin);
+}
+
+// Sphere::hit_by (sphere.h:45-96) returning the accepted root through t.
+// Before the exact sqrt and divisions, a coarse bound (hardware rsq, error <= 2^-23 relative;
+// margins of 2^-12 on every term) proves "both roots >= t_max" or "both roots <= t_min" for
+// spheres that cannot be accepted; only those are skipped, so the accepted roots are exactly the
+// reference's. NaN/inf anywhere makes the bound inconclusive and falls through to the exact test.
 __device__ __forceinline__ bool hit_sphere(const DevSphere& sp, const double o[3], const double d[3],
                                            double a, double tmin, double tmax, double& t) {
     double ocx = o[0] - sp.c[0], ocy = o[1] - sp.c[1], ocz = o[2] - sp.c[2];
@@ -134,6 +168,13 @@ __device__ __forceinline__ bool hit_sphere(const DevSphere& sp, const double o[3
     double c = (ocx * ocx + ocy * ocy + ocz * ocz) - sp.r * sp.r;
     double disc = b * b - a * c;
     if (disc < 0) return false;
+    {
+        const double sqa = disc * __builtin_amdgcn_rsq(disc);      // ~sqrt(disc)
+        const double m = (fabs(b) + sqa) * 0x1p-12;                // covers every rounding error
+        const bool beyond = (-b - sqa) - m > tmax * a * (1 + 0x1p-30);   // r1 > tmax, so r2 too
+        const bool before = (-b + sqa) + m < tmin * a * (1 - 0x1p-30);   // r2 < tmin, so r1 too
+        if (beyond || before) return false;
+    }
     double sq = sqrt(disc);
     double root = (-b - sq) / a;
     if (!(tmin < root && root < tmax)) {
@@ -223,7 +264,7 @@ __device__ __forceinline__ bool trace(const SceneView& S, Stack<SE>& st, const d
                                       const double d[3], double tmin, double& tmax,
                                       uint32_t& hit_ref, Counters& ctr) {
     const double inv[3] = {1 / d[0], 1 / d[1], 1 / d[2]};
-    const int neg[3] = {d[0] < 0, d[1] < 0, d[2] < 0};
+    const uint32_t neg = (d[0] < 0 ? 1u : 0u) | (d[1] < 0 ? 2u : 0u) | (d[2] < 0 ? 4u : 0u);
     const double a = d[0] * d[0] + d[1] * d[1] + d[2] * d[2];  // dot(ray.dir, ray.dir)
     bool found = false;
     int sp = 0;
@@ -232,16 +273,16 @@ __device__ __forceinline__ bool trace(const SceneView& S, Stack<SE>& st, const d
     while (!done) {
         uint32_t first = 0, count = 0;
         while (true) {  // interior walk until a leaf is entered
-            const DevNode& n = S.nodes[cur];
+            const NodeRegs n = load_node(S.nodes, cur);
             if (COUNT) ctr.nodes++;
-            const bool enter = (n.flags & kNodeAlways) || slab(n, o, inv, neg, tmin, tmax);
+            const bool enter = slab(n, o, inv, neg, tmin, tmax) | ((n.flags & kNodeAlways) != 0);
             if (enter) {
                 if (n.count > 0) {
                     first = n.index;
                     count = n.count;
                     break;
                 }
-                if (neg[n.axis]) {
+                if ((neg >> n.axis) & 1u) {
                     st.put(sp++, cur + 1);
                     cur = n.index;
                 } else {
@@ -281,16 +322,125 @@ __device__ __forceinline__ bool trace(const SceneView& S, Stack<SE>& st, const d
     return found;
 }
 
+// Per-lane traversal state of the render kernel's current ray. The kernel advances it one BVH
+// node per iteration (walk) and tests an entered leaf's primitives in a separate, batched phase;
+// per lane the sequence of node tests and primitive tests is exactly trace()'s, i.e. the
+// reference's BVH::hit_by.
+enum : uint32_t { kWalk = 0, kLeaf = 1, kDone = 2, kIdle = 3 };
+
+struct Trav {
+    double inv[3];
+    double a;        // dot(d, d)
+    double tmax;
+    uint32_t cur, sp, ref;
+    uint32_t first, count;  // pending leaf
+    uint32_t neg;    // bit k: d[k] < 0
+    uint32_t state;
+    bool found;
+};
+
+__device__ __forceinline__ void trav_init(const double d[3], Trav& R) {
+    R.inv[0] = 1 / d[0];
+    R.inv[1] = 1 / d[1];
+    R.inv[2] = 1 / d[2];
+    R.a = d[0] * d[0] + d[1] * d[1] + d[2] * d[2];
+    R.tmax = __builtin_inf();
+    R.cur = 0;
+    R.sp = 0;
+    R.ref = 0;
+    R.first = 0;
+    R.count = 0;
+    R.neg = (d[0] < 0 ? 1u : 0u) | (d[1] < 0 ? 2u : 0u) | (d[2] < 0 ? 4u : 0u);
+    R.state = kWalk;
+    R.found = false;
+}
+
+// one node of the DFS (bvh.h:617-712 loop body without the leaf's primitive loop)
+template <typename SE, bool COUNT>
+__device__ __forceinline__ void walk_step(const SceneView& S, Stack<SE>& st, const double o[3],
+                                          double tmin, Trav& R, Counters& ctr) {
+    const NodeRegs n = load_node(S.nodes, R.cur);
+    if (COUNT) ctr.nodes++;
+    const bool enter = slab(n, o, R.inv, R.neg, tmin, R.tmax) | ((n.flags & kNodeAlways) != 0);
+    if (enter) {
+        if (n.count > 0) {
+            R.first = n.index;
+            R.count = n.count;
+            R.state = kLeaf;
+        } else if ((R.neg >> n.axis) & 1u) {
+            st.put(R.sp++, R.cur + 1);
+            R.cur = n.index;
+        } else {
+            st.put(R.sp++, n.index);
+            R.cur = R.cur + 1;
+        }
+    } else if (R.sp == 0) {
+        R.state = kDone;
+    } else {
+        R.cur = st.get(--R.sp);
+    }
+}
+
+// the entered leaf's primitives in order (bvh.h:635-652), then "return" to the DFS.
+// Sphere-only scenes store spheres in slot order, so the slot indexes them directly and the next
+// sphere is loaded while the current one is tested.
+template <typename SE, bool COUNT>
+__device__ __forceinline__ void leaf_step(const SceneView& S, Stack<SE>& st, const double o[3],
+                                          const double d[3], double tmin, bool sphere_only,
+                                          Trav& R, Counters& ctr) {
+    const uint32_t end = R.first + R.count;
+    if (sphere_only) {
+        DevSphere cur = S.spheres[R.first];
+        for (uint32_t i = R.first; i < end; ++i) {
+            const DevSphere nxt = S.spheres[i + 1 < end ? i + 1 : i];
+            if (COUNT) ctr.sphere_tests++;
+            double t;
+            if (hit_sphere(cur, o, d, R.a, tmin, R.tmax, t)) {
+                R.tmax = t;
+                R.ref = i;
+                R.found = true;
+            }
+            cur = nxt;
+        }
+    } else {
+        for (uint32_t i = R.first; i < end; ++i) {
+            const uint32_t ref = S.refs[i];
+            double t;
+            bool h;
+            if (ref & kRefQuad) {
+                if (COUNT) ctr.quad_tests++;
+                h = hit_quad(S.quads[ref & ~kRefQuad], o, d, tmin, R.tmax, t);
+            } else {
+                if (COUNT) ctr.sphere_tests++;
+                h = hit_sphere(S.spheres[ref], o, d, R.a, tmin, R.tmax, t);
+            }
+            if (h) {
+                R.tmax = t;
+                R.ref = ref;
+                R.found = true;
+            }
+        }
+    }
+    if (R.sp == 0) {
+        R.state = kDone;
+    } else {
+        R.cur = st.get(--R.sp);
+        R.state = kWalk;
+    }
+}
+
 __device__ __forceinline__ uint32_t owned_row(const Work& w, uint32_t k) {
     uint32_t blk = k / w.row_block, in = k % w.row_block;
     return (blk * w.tile_count + w.tile_index) * w.row_block + in;
 }
 
-// State of one lane's current path: the ray, the throughput, the radiance gathered so far and the
-// bounces left (ray_color's depth_left, camera.h:207-213).
+// State of one lane's current path: the ray, the throughput and the bounces left (ray_color's
+// depth_left, camera.h:207-213). Emission enters a path only where it ends (a DiffuseLight never
+// scatters, a miss returns the background), so no running radiance is kept: the terminal
+// T * (emit | background) goes straight into the pixel's sum.
 struct Path {
     double o[3], d[3];
-    double T[3], L[3];
+    double T[3];
     uint32_t depth;
     uint32_t rng;
 };
@@ -319,21 +469,20 @@ __device__ __forceinline__ void start_path(const CamView& C, uint32_t row, uint3
         const double sample = (center + C.pdx[k] * ux) + C.pdy[k] * uy;
         P.d[k] = sample - P.o[k];
         P.T[k] = 1;
-        P.L[k] = 0;
     }
     P.depth = C.max_depth;
     P.rng = rng;
 }
 
-// One level of ray_color (camera.h:205-258) after the closest-hit query: gathers emission or
-// background into L, scatters (material.h:64-263) into the next ray. Returns true when the path
-// has ended (miss, light, absorption).
+// One level of ray_color (camera.h:205-258) after the closest-hit query: scatters
+// (material.h:64-263) into the next ray, or ends the path adding T * (background | emission) to
+// acc. Returns true when the path has ended (miss, light, absorption).
 __device__ __forceinline__ bool shade(const SceneView& S, const CamView& C, Path& P, bool hit,
-                                      uint32_t ref, double t) {
+                                      uint32_t ref, double t, double acc[3]) {
     if (!hit) {
-        P.L[0] += P.T[0] * C.bg[0];
-        P.L[1] += P.T[1] * C.bg[1];
-        P.L[2] += P.T[2] * C.bg[2];
+        acc[0] = acc[0] + P.T[0] * C.bg[0];
+        acc[1] = acc[1] + P.T[1] * C.bg[1];
+        acc[2] = acc[2] + P.T[2] * C.bg[2];
         return true;
     }
     double p[3], n[3];
@@ -389,9 +538,9 @@ __device__ __forceinline__ bool shade(const SceneView& S, const CamView& C, Path
             nd[2] = pz + n[2] * s;
         }
     } else {  // DiffuseLight: emits, never scatters (material.h:248-263)
-        P.L[0] += P.T[0] * M.emit[0];
-        P.L[1] += P.T[1] * M.emit[1];
-        P.L[2] += P.T[2] * M.emit[2];
+        acc[0] = acc[0] + P.T[0] * M.emit[0];
+        acc[1] = acc[1] + P.T[1] * M.emit[1];
+        acc[2] = acc[2] + P.T[2] * M.emit[2];
         return true;
     }
     if (kind != CRT_DIELECTRIC) {  // attenuation = intrinsic colour (dielectric: 1)
@@ -413,15 +562,34 @@ __device__ __forceinline__ void stage_lds(unsigned char* dst, const void* src, u
 }
 
 // The render kernel. Thread -> (sample chunk, pixel); each wave starts on one 8x8 pixel tile.
-// A lane loops over its chunk's samples with path regeneration: one iteration = one ray segment
-// (closest hit + shade); when a path ends the lane starts its next sample at once, so a wave is
-// never held by its longest path. Samples are summed in sample order into partial[chunk][pixel].
+// Persistent per-lane state machine (WALK -> LEAF -> ... -> DONE -> shade -> WALK): every
+// iteration each walking lane visits one BVH node; lanes that entered a leaf park until at least
+// kLeafBatch of them hold one (or nobody walks), then test their leaves together; lanes whose ray
+// is finished park until kShadeBatch of them are finished (or nobody traverses), then shade
+// together, and a finished path starts the lane's next sample at once (path regeneration). So
+// the expensive leaf and shading code runs with many lanes active while the others keep
+// walking, and a wave is never held by its slowest ray or path.
+// Samples are summed in sample order into partial[chunk][pixel].
 // LSCENE: nodes, primitive refs, spheres and parallelograms are staged in LDS first.
+#ifndef CRT_WAVES_PER_EU
+#define CRT_WAVES_PER_EU 5
+#endif
+#ifndef CRT_SHADE_BATCH
+#define CRT_SHADE_BATCH 32
+#endif
+#ifndef CRT_LEAF_BATCH
+#define CRT_LEAF_BATCH 24
+#endif
+#ifndef CRT_SCHED
+#define CRT_SCHED 0  // 0: traversal rounds + batched shading; 1: node-level state machine
+#endif
+constexpr int kShadeBatch = CRT_SHADE_BATCH;
+constexpr int kLeafBatch = CRT_LEAF_BATCH;
+
 template <typename SE, bool GSTACK, bool LSCENE, bool COUNT>
-__global__ __launch_bounds__(kBlock) void render_kernel(SceneView Sg, CamView C, Work W,
-                                                        double* __restrict__ partial,
-                                                        SE* __restrict__ gstack,
-                                                        Counters* __restrict__ counters) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRT_WAVES_PER_EU, 8))) void render_kernel(
+    SceneView Sg, CamView C, Work W, double* __restrict__ partial, SE* __restrict__ gstack,
+    Counters* __restrict__ counters) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     SceneView S = Sg;
     if (LSCENE) {
@@ -439,55 +607,111 @@ __global__ __launch_bounds__(kBlock) void render_kernel(SceneView Sg, CamView C,
     const uint64_t wave = (static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x) >> 6;
     const uint32_t chunk = static_cast<uint32_t>(wave / W.tiles);
     const uint32_t tile = static_cast<uint32_t>(wave % W.tiles);
-    Counters ctr{0, 0, 0, 0};
+    Counters ctr{};
+    const unsigned long long t_start = COUNT ? wall_clock64() : 0;
     const uint32_t tx = tile % W.tiles_x, ty = tile / W.tiles_x;
     const uint32_t col = tx * 8 + (lane & 7);
     const uint32_t k = ty * 8 + (lane >> 3);
-    if (chunk < W.chunks && col < C.w && k < W.owned_rows) {
-        const uint32_t row = owned_row(W, k);
-        Stack<SE> st;
-        if (GSTACK) {
-            st.base = gstack + (static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x);
-            st.stride = gridDim.x * kBlock;
-        } else {
-            st.base = reinterpret_cast<SE*>(smem + W.lds_stack) + threadIdx.x;
-            st.stride = kBlock;
-        }
-        const uint32_t pixel = row * C.w + col;
-        uint32_t s = chunk * W.chunk_len;
-        const uint32_t s_end = min(C.spp, s + W.chunk_len);
-        double acc[3] = {0, 0, 0};
-        Path P;
+    const bool valid = chunk < W.chunks && col < C.w && k < W.owned_rows;
+    Stack<SE> st;
+    if (GSTACK) {
+        st.base = gstack + (static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x);
+        st.stride = gridDim.x * kBlock;
+    } else {
+        st.base = reinterpret_cast<SE*>(smem + W.lds_stack) + threadIdx.x;
+        st.stride = kBlock;
+    }
+    const uint32_t row = valid ? owned_row(W, k) : 0;
+    const uint32_t pixel = row * C.w + col;
+    uint32_t s = chunk * W.chunk_len;
+    const uint32_t s_end = valid ? min(C.spp, s + W.chunk_len) : s;
+    double acc[3] = {0, 0, 0};
+    Path P;
+    Trav R;
+    R.state = kIdle;
+    // max_depth == 0: ray_color returns RGB::zero() for every sample (camera.h:211-213)
+    if (valid && C.max_depth > 0 && s < s_end) {
         start_path(C, row, col, sample_seed(C.base_seed, pixel, s), P);
+        trav_init(P.d, R);
+        if (COUNT) ctr.rays++;
+    }
+    unsigned long long cw = 0, cl = 0, cs = 0;
+    while (true) {
+#if CRT_SCHED == 0
+        // traversal rounds (walk to the next entered leaf, test it) until enough lanes hold a
+        // finished ray, or none is traversing
         while (true) {
-            bool ended = true;
-            if (P.depth > 0) {
-                if (COUNT) ctr.rays++;
-                double tmax = __builtin_inf();
-                uint32_t ref = 0;
-                const bool hit = trace<SE, COUNT>(S, st, P.o, P.d, C.t_min, tmax, ref, ctr);
-                ended = shade(S, C, P, hit, ref, tmax);
-            }  // depth exhausted: ray_color returns RGB::zero() (camera.h:211-213)
-            if (ended) {
-                acc[0] = acc[0] + P.L[0];
-                acc[1] = acc[1] + P.L[1];
-                acc[2] = acc[2] + P.L[2];
-                if (++s >= s_end) break;
-                start_path(C, row, col, sample_seed(C.base_seed, pixel, s), P);
+            if (COUNT) cw -= wall_clock64();
+            while (R.state == kWalk) walk_step<SE, COUNT>(S, st, P.o, C.t_min, R, ctr);
+            if (COUNT) cw += wall_clock64();
+            if (COUNT) cl -= wall_clock64();
+            if (R.state == kLeaf) leaf_step<SE, COUNT>(S, st, P.o, P.d, C.t_min, W.sphere_only != 0, R, ctr);
+            if (COUNT) cl += wall_clock64();
+            const uint64_t pending = __ballot(R.state == kWalk);
+            const uint64_t finished = __ballot(R.state == kDone);
+            if (pending == 0 || __popcll(finished) >= kShadeBatch) break;
+        }
+        const uint64_t m_done = __ballot(R.state == kDone);
+        if (m_done == 0) break;  // every lane idle: the chunk is finished
+        {
+#else
+        // walk: one BVH node for every walking lane
+        if (COUNT) cw -= wall_clock64();
+        if (R.state == kWalk) walk_step<SE, COUNT>(S, st, P.o, C.t_min, R, ctr);
+        if (COUNT) cw += wall_clock64();
+        const uint64_t m_walk = __ballot(R.state == kWalk);
+        const uint64_t m_leaf = __ballot(R.state == kLeaf);
+        // leaf batch: once enough lanes hold an entered leaf, or nobody walks any more
+        if (m_leaf != 0 && (__popcll(m_leaf) >= kLeafBatch || m_walk == 0)) {
+            if (COUNT) cl -= wall_clock64();
+            if (R.state == kLeaf) leaf_step<SE, COUNT>(S, st, P.o, P.d, C.t_min, W.sphere_only != 0, R, ctr);
+            if (COUNT) cl += wall_clock64();
+        }
+        const uint64_t m_busy = __ballot(R.state == kWalk || R.state == kLeaf);
+        const uint64_t m_done = __ballot(R.state == kDone);
+        if (m_done == 0 && m_busy == 0) break;  // every lane idle: the chunk is finished
+        // shade batch: once enough rays are finished, or nobody traverses any more
+        if (m_done != 0 && (__popcll(m_done) >= kShadeBatch || m_busy == 0)) {
+#endif
+            if (COUNT) cs -= wall_clock64();
+            if (R.state == kDone) {
+                bool ended = shade(S, C, P, R.found, R.ref, R.tmax, acc);
+                // a scattered ray with no bounce left returns RGB::zero() (camera.h:211-213)
+                if (!ended && P.depth == 0) ended = true;
+                if (ended) {
+                    if (++s >= s_end) R.state = kIdle;
+                    else start_path(C, row, col, sample_seed(C.base_seed, pixel, s), P);
+                }
+                if (R.state != kIdle) {
+                    trav_init(P.d, R);
+                    if (COUNT) ctr.rays++;
+                }
             }
+            if (COUNT) cs += wall_clock64();
         }
-        if (!COUNT) {
-            double* dst = partial + (static_cast<size_t>(chunk) * C.h * C.w + pixel) * 3;
-            dst[0] = acc[0];
-            dst[1] = acc[1];
-            dst[2] = acc[2];
-        }
+    }
+    if (COUNT) {
+        ctr.cyc_walk = cw;
+        ctr.cyc_leaf = cl;
+        ctr.cyc_shade = cs;
+    }
+    if (valid && !COUNT) {
+        double* dst = partial + (static_cast<size_t>(chunk) * C.h * C.w + pixel) * 3;
+        dst[0] = acc[0];
+        dst[1] = acc[1];
+        dst[2] = acc[2];
     }
     if (COUNT) {
         atomicAdd(&counters->rays, ctr.rays);
         atomicAdd(&counters->nodes, ctr.nodes);
         atomicAdd(&counters->sphere_tests, ctr.sphere_tests);
         atomicAdd(&counters->quad_tests, ctr.quad_tests);
+        if (lane == 0) {  // per-wave phase times (the wave executes each phase as one)
+            atomicAdd(&counters->cyc_walk, ctr.cyc_walk);
+            atomicAdd(&counters->cyc_leaf, ctr.cyc_leaf);
+            atomicAdd(&counters->cyc_shade, ctr.cyc_shade);
+            atomicAdd(&counters->cyc_total, wall_clock64() - t_start);
+        }
     }
 }
 
@@ -764,6 +988,10 @@ static int launch_render(const crt_scene* s, int device, const crt_camera* cam, 
         count_stats->sphere_tests = h.sphere_tests;
         count_stats->parallelogram_tests = h.quad_tests;
         count_stats->kernel_ms = ms;
+        count_stats->ticks_walk = h.cyc_walk;
+        count_stats->ticks_leaf = h.cyc_leaf;
+        count_stats->ticks_shade = h.cyc_shade;
+        count_stats->ticks_total = h.cyc_total;
     }
     return CRT_OK;
 }
@@ -834,6 +1062,7 @@ int device_render(const crt_scene* s, int device, const crt_camera* cam, const c
     W.tiles_x = (cam->image_w + 7) / 8;
     W.tiles_y = (W.owned_rows + 7) / 8;
     W.tiles = W.tiles_x * W.tiles_y;
+    W.sphere_only = (s->quads.empty() && !s->spheres.empty()) ? 1u : 0u;
     hipStream_t st = static_cast<hipStream_t>(stream);
     if (count_stats) HIP_TRY(hipStreamCreate(&st));
     int r;

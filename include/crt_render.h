@@ -160,6 +160,9 @@ typedef struct crt_render_stats {
     uint64_t sphere_tests;
     uint64_t parallelogram_tests;
     double kernel_ms;
+    /* wave-time breakdown of the instrumented pass (sum over waves, 100 MHz ticks): interior
+     * BVH walk, leaf primitive tests, shading + path regeneration, whole wave lifetime */
+    uint64_t ticks_walk, ticks_leaf, ticks_shade, ticks_total;
 } crt_render_stats;
 
 /* ---- entry points ---------------------------------------------------------------------- */
