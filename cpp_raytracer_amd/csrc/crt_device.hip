@@ -355,30 +355,46 @@ __device__ __forceinline__ void trav_init(const double d[3], Trav& R) {
     R.found = false;
 }
 
-// one node of the DFS (bvh.h:617-712 loop body without the leaf's primitive loop)
+// one node of the DFS (bvh.h:617-712 loop body without the leaf's primitive loop), branch-free:
+// the node's bounds are loaded by per-lane address (x[neg] / x[!neg] of aabb.h:141-159), its
+// index/count/axis/flags and the stack top are loaded in the same batch, and the push / pop /
+// leaf / done outcomes are selected rather than branched to (only the push is a masked store).
 template <typename SE, bool COUNT>
 __device__ __forceinline__ void walk_step(const SceneView& S, Stack<SE>& st, const double o[3],
                                           double tmin, Trav& R, Counters& ctr) {
-    const NodeRegs n = load_node(S.nodes, R.cur);
+    const uint32_t cur = R.cur, sp = R.sp;
+    const double* b = reinterpret_cast<const double*>(S.nodes + cur);
+    const uint32_t nx = R.neg & 1u, ny = (R.neg >> 1) & 1u, nz = (R.neg >> 2) & 1u;
+    const double bx0 = b[0 + nx], bx1 = b[1 - nx];
+    const double by0 = b[2 + ny], by1 = b[3 - ny];
+    const double bz0 = b[4 + nz], bz1 = b[5 - nz];
+    const uint4 meta = reinterpret_cast<const uint4*>(S.nodes + cur)[3];  // index count axis flags
+    const uint32_t top = st.get(sp > 0 ? static_cast<int>(sp) - 1 : 0);  // speculative pop
     if (COUNT) ctr.nodes++;
-    const bool enter = slab(n, o, R.inv, R.neg, tmin, R.tmax) | ((n.flags & kNodeAlways) != 0);
-    if (enter) {
-        if (n.count > 0) {
-            R.first = n.index;
-            R.count = n.count;
-            R.state = kLeaf;
-        } else if ((R.neg >> n.axis) & 1u) {
-            st.put(R.sp++, R.cur + 1);
-            R.cur = n.index;
-        } else {
-            st.put(R.sp++, n.index);
-            R.cur = R.cur + 1;
-        }
-    } else if (R.sp == 0) {
-        R.state = kDone;
-    } else {
-        R.cur = st.get(--R.sp);
-    }
+    double xtmin = (bx0 - o[0]) * R.inv[0];
+    double xtmax = (bx1 - o[0]) * R.inv[0];
+    const double ytmin = (by0 - o[1]) * R.inv[1];
+    const double ytmax = (by1 - o[1]) * R.inv[1];
+    const double ztmin = (bz0 - o[2]) * R.inv[2];
+    const double ztmax = (bz1 - o[2]) * R.inv[2];
+    const bool c1 = !(xtmin > ytmax || ytmin > xtmax);
+    if (ytmin > xtmin) xtmin = ytmin;
+    if (ytmax < xtmax) xtmax = ytmax;
+    const bool c2 = !(xtmin > ztmax || ztmin > xtmax);
+    if (ztmin > xtmin) xtmin = ztmin;
+    if (ztmax < xtmax) xtmax = ztmax;
+    const bool enter = (c1 & c2 & (xtmin < R.tmax) & (xtmax > tmin)) |
+                       ((meta.w & kNodeAlways) != 0);
+    const bool leaf = enter && meta.y > 0;
+    const bool inner = enter && meta.y == 0;
+    const bool far_first = (R.neg >> meta.z) & 1u;
+    if (inner) st.put(static_cast<int>(sp), far_first ? cur + 1 : meta.x);
+    const bool pop = !enter && sp > 0;
+    R.cur = inner ? (far_first ? meta.x : cur + 1) : (pop ? top : cur);
+    R.sp = inner ? sp + 1 : (pop ? sp - 1 : sp);
+    R.first = leaf ? meta.x : R.first;
+    R.count = leaf ? meta.y : R.count;
+    R.state = leaf ? kLeaf : ((!enter && sp == 0) ? kDone : kWalk);
 }
 
 // the entered leaf's primitives in order (bvh.h:635-652), then "return" to the DFS.
