@@ -1,0 +1,90 @@
+"""Pin the C oracle (oracle/crt_oracle.c) to the REFERENCE's own outputs (tests/golden, produced
+by oracle/_ref from /root/reference): bit-for-bit on every fixture. The oracle is then the CPU
+checker for cases with no golden (random scenes, the port CPU baseline)."""
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, load_npz
+
+sys.path.insert(0, str(ROOT / "oracle"))
+import crt_oracle_py as orc  # noqa: E402
+
+
+def scene_for(crt, meta):
+    from cpp_raytracer_amd import camera_with
+    d = crt.SceneData.named(meta["scene"], meta["seed"])
+    d.camera = camera_with(d.camera, **meta["camera"])
+    return d
+
+
+@pytest.mark.parametrize("case", ["config1", "rtow_crop", "rtow_glass_crop", "cornell_crop",
+                                  "cornell_empty_small", "parallelograms_small", "lights_crop",
+                                  "christmas_crop"])
+def test_oracle_render_bit_exact(crt, golden_meta, case):
+    meta = golden_meta["renders"][case]
+    want = load_npz(f"render_{case}.npz")["rgb"]
+    got = orc.render(scene_for(crt, meta), meta["base_seed"], threads=4,
+                     crop=tuple(meta["crop"]) if meta["crop"] else None)
+    assert got.shape == want.shape
+    assert np.array_equal(got.view(np.uint64), want.view(np.uint64)), \
+        f"{case}: max err {np.abs(got - want).max()}"
+
+
+@pytest.mark.parametrize("case", ["rtow_samples", "cornell_samples"])
+def test_oracle_samples_bit_exact(crt, golden_meta, case):
+    meta = golden_meta["renders"][case]
+    want = load_npz(f"samples_{case}.npz")["samples"]
+    _, got = orc.render(scene_for(crt, meta), meta["base_seed"], threads=4, crop=tuple(meta["crop"]),
+                        samples=True)
+    assert np.array_equal(got.view(np.uint64), want.view(np.uint64))
+
+
+@pytest.mark.parametrize("name,seed", [("config1", None), ("rtow_final", 42), ("cornell", None),
+                                       ("parallelograms", None), ("christmas_tree", None),
+                                       ("bvh_pathological", None), ("rtow_final_lights", None)])
+def test_oracle_bvh_bit_exact(crt, name, seed):
+    g = load_npz(f"bvh_{name}.npz")
+    nodes, order = orc.bvh(crt.SceneData.named(name, seed))
+    assert np.array_equal(nodes["bounds"].view(np.uint64), g["bounds"].view(np.uint64))
+    for k in ("index", "count", "axis"):
+        assert np.array_equal(nodes[k], g[k])
+    assert np.array_equal(order, g["order"])
+
+
+@pytest.mark.parametrize("name,seed", [("rtow_final", 42), ("cornell", None), ("christmas_tree", None)])
+def test_oracle_hits_bit_exact(crt, name, seed):
+    g = load_npz(f"hits_{name}.npz")
+    rays, ref = g["rays"], g["hits"]
+    h = orc.hits(crt.SceneData.named(name, seed), rays)
+    miss = ref[:, 7] == -1
+    assert np.array_equal(h["prim"] == -1, miss)
+    hit = ~miss
+    assert np.array_equal(h["prim"][hit], ref[hit, 7].astype(np.int32))
+    assert np.array_equal(h["t"][hit].view(np.uint64), ref[hit, 0].view(np.uint64))
+    assert np.array_equal(h["normal"][hit].view(np.uint64), ref[hit, 4:7].view(np.uint64))
+
+
+def test_oracle_camera_matches_reference(crt, golden_meta):
+    for name, ref in golden_meta["cameras"].items():
+        cam = orc.camera(crt.SceneData.named(name, golden_meta["scenes"][name]["seed"]).camera)
+        assert [cam.pixel00[i] for i in range(3)] == ref["pixel00"]
+        assert [cam.pixel_delta_y[i] for i in range(3)] == ref["pixel_delta_y"]
+        assert [cam.defocus_disk_x[i] for i in range(3)] == ref["defocus_disk_x"]
+
+
+def test_oracle_seed_matches_library(crt):
+    for b, p, s in [(0, 0, 0), (7, 12345, 499), (2**32 - 1, 2**31, 9999)]:
+        assert orc.lib().oracle_sample_seed(b, p, s) == crt.sample_seed(b, p, s)
+
+
+def test_oracle_bvh_matches_library_on_big_scene(crt):
+    """Size-independent property at scale: the oracle's BVH equals the library's on the 4202-prim
+    christmas tree and a 25k-sphere random field (no golden needed: two independent builds)."""
+    import hashlib
+    d = crt.SceneData.named("christmas_tree")
+    on, oo = orc.bvh(d)
+    ln, lo = crt.GpuScene(d).export_bvh()
+    assert hashlib.sha256(on.tobytes()).digest() == hashlib.sha256(ln.tobytes()).digest()
+    assert np.array_equal(oo, lo)
