@@ -600,7 +600,7 @@ __device__ __forceinline__ void stage_lds(unsigned char* dst, const void* src, u
 #define CRT_SCHED 0  // 0: traversal rounds + batched shading; 1: node-level state machine
 #endif
 constexpr int kShadeBatch = CRT_SHADE_BATCH;
-constexpr int kLeafBatch = CRT_LEAF_BATCH;
+[[maybe_unused]] constexpr int kLeafBatch = CRT_LEAF_BATCH;
 
 template <typename SE, bool GSTACK, bool LSCENE, bool COUNT>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRT_WAVES_PER_EU, 8))) void render_kernel(
@@ -712,7 +712,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRT_WAVE
         ctr.cyc_shade = cs;
     }
     if (valid && !COUNT) {
-        double* dst = partial + (static_cast<size_t>(chunk) * C.h * C.w + pixel) * 3;
+        const size_t owned_pixel = static_cast<size_t>(k) * C.w + col;
+        double* dst = partial + (static_cast<size_t>(chunk) * W.owned_rows * C.w + owned_pixel) * 3;
         dst[0] = acc[0];
         dst[1] = acc[1];
         dst[2] = acc[2];
@@ -736,16 +737,17 @@ __global__ __launch_bounds__(256) void resolve_kernel(const double* __restrict__
                                                       double* __restrict__ out, Work W, uint32_t w,
                                                       uint32_t h, double inv_spp) {
     const uint64_t i = static_cast<uint64_t>(blockIdx.x) * 256 + threadIdx.x;
-    if (i >= static_cast<uint64_t>(W.owned_rows) * w) return;
+    const uint64_t owned = static_cast<uint64_t>(W.owned_rows) * w;
+    if (i >= owned) return;
     const uint32_t k = static_cast<uint32_t>(i / w), col = static_cast<uint32_t>(i % w);
     const uint32_t row = owned_row(W, k);
     const size_t pix = static_cast<size_t>(row) * w + col;
-    const size_t plane = static_cast<size_t>(h) * w * 3;
-    double r = partial[pix * 3 + 0], g = partial[pix * 3 + 1], b = partial[pix * 3 + 2];
+    const size_t plane = owned * 3;
+    double r = partial[i * 3 + 0], g = partial[i * 3 + 1], b = partial[i * 3 + 2];
     for (uint32_t c = 1; c < W.chunks; ++c) {
-        r = r + partial[c * plane + pix * 3 + 0];
-        g = g + partial[c * plane + pix * 3 + 1];
-        b = b + partial[c * plane + pix * 3 + 2];
+        r = r + partial[c * plane + i * 3 + 0];
+        g = g + partial[c * plane + i * 3 + 1];
+        b = b + partial[c * plane + i * 3 + 2];
     }
     out[pix * 3 + 0] = r * inv_spp;
     out[pix * 3 + 1] = g * inv_spp;
@@ -916,39 +918,22 @@ static size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
 constexpr size_t kLdsSceneBudget = 40 * 1024;  // scene + stack; keeps >= 3 blocks (12 waves)/CU
 constexpr size_t kLdsStackBudget = 32 * 1024;
 
-template <typename SE, bool GSTACK, bool LSCENE, bool COUNT>
-static const void* kernel_ptr() {
-    return reinterpret_cast<const void*>(dev::render_kernel<SE, GSTACK, LSCENE, COUNT>);
-}
-
-// resident threads of a render-kernel variant on this device (for the sample-chunk split)
-static size_t resident_threads(const void* fn, size_t lds, int device) {
-    int blocks = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fn, dev::kBlock, lds) != hipSuccess ||
-        blocks <= 0)
-        blocks = 2;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
-        cus = 256;
-    return static_cast<size_t>(blocks) * cus * dev::kBlock;
-}
-
 template <typename SE, bool GSTACK, bool LSCENE>
 static int launch_render(const crt_scene* s, int device, const crt_camera* cam, const dev::Work& w0,
                          size_t lds, double* d_rgb, hipStream_t stream, crt_render_stats* count_stats) {
     const DeviceCopy& c = s->dev[device];
     dev::Work W = w0;
     const uint64_t pixels = static_cast<uint64_t>(W.owned_rows) * cam->image_w;
-    const size_t resident = resident_threads(kernel_ptr<SE, GSTACK, LSCENE, false>(), lds, device);
-    // enough threads for ~8 rounds of residency so block-level dynamic dispatch balances rows of
-    // very different cost; never split below 1 sample per thread
-    uint64_t want = (8 * static_cast<uint64_t>(resident) + pixels - 1) / std::max<uint64_t>(1, pixels);
-    W.chunks = static_cast<uint32_t>(std::min<uint64_t>(std::max<uint64_t>(1, want), cam->samples_per_pixel));
-    W.chunk_len = (cam->samples_per_pixel + W.chunks - 1) / W.chunks;
-    W.chunks = (cam->samples_per_pixel + W.chunk_len - 1) / W.chunk_len;
+    // Sample chunks: a function of spp ONLY, so every pixel's sum is grouped identically whatever
+    // the tiling / number of GPUs (bit-identical frames for 1..N devices). 64-sample chunks keep
+    // ~8 chunks per pixel at BASELINE spp (enough threads for dynamic balance); at most 64 chunks.
+    const uint32_t spp = cam->samples_per_pixel;
+    W.chunk_len = std::max<uint32_t>(64, (spp + 63) / 64);
+    W.chunks = (spp + W.chunk_len - 1) / W.chunk_len;
     const uint64_t waves = static_cast<uint64_t>(W.tiles) * W.chunks;
     const uint64_t blocks = (waves * 64 + dev::kBlock - 1) / dev::kBlock;
     if (blocks > 0x7fffffffull) return fail(CRT_E_INVALID, "frame too large for one launch");
-    const size_t plane = static_cast<size_t>(cam->image_h) * cam->image_w * 3;
+    const size_t plane = static_cast<size_t>(pixels) * 3;  // partials indexed by owned pixel
 
     double* partial = nullptr;
     SE* gstack = nullptr;
@@ -1032,7 +1017,7 @@ static int dispatch_render(const crt_scene* s, int device, const crt_camera* cam
         W.lds_stack = W.lds_quads + W.bytes_quads;
         return launch_render<SE, false, true>(s, device, cam, W, scene_bytes + stack_bytes, d_rgb, st, count_stats);
     }
-    if (stack_bytes <= kLdsStackBudget) {
+    if (stack_bytes <= kLdsStackBudget && std::getenv("CRT_FORCE_GSTACK") == nullptr) {
         W.lds_stack = 0;
         return launch_render<SE, false, false>(s, device, cam, W, stack_bytes, d_rgb, st, count_stats);
     }
