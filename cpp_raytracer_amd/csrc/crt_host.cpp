@@ -768,7 +768,11 @@ static bool build_named(const std::string& name, RefRng& R, SceneOut& S) {
                 if (i == 0) ry = apex;
                 double rad = (20 - ry) * ratio;
                 double ang = R.rd(0, 2 * std::numbers::pi);
-                V3 cc{rad * std::sin(ang), ry, rad * std::cos(ang)};
+                // a g++ -O2/-O3 build fuses std::sin + std::cos of one angle into glibc's
+                // sincos(), which can differ from sin() in the last bit: call it explicitly
+                double sn, cs;
+                ::sincos(ang, &sn, &cs);
+                V3 cc{rad * sn, ry, rad * cs};
                 double sr = R.rd(0.25, 0.45);
                 if (too_close(cc, sr)) continue;
                 // ms<Metal>(colors[rand_int(0, 5)], rand_double(0, 0.1)): fuzz drawn first

@@ -1,0 +1,222 @@
+// Drop-in for the reference's base/camera.h. Same fluent setters and render() entry points;
+// render runs the per-pixel / per-sample loop on the MI355X GPUs of this process through the C ABI
+// (crt_render: rows dealt to every visible device in 16-row blocks, tiles gathered to the host).
+// There is no CPU fallback: without a GPU render prints the reason and exits, as the reference does
+// on its own errors.
+//
+// RNG: the reference seeds one LCG per OpenMP thread (rand_util.h:106); here each (pixel, sample)
+// gets its own state crt_sample_seed(base, pixel, sample), with base = one next_seed() of
+// SeedSeqGenerator per render, so output does not depend on scheduling or device count.
+#ifndef CAMERA_H
+#define CAMERA_H
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <iostream>
+#include <numbers>
+#include <optional>
+#include <string>
+#include <type_traits>
+#include <vector>
+
+#include "acceleration/bvh.h"
+#include "math/ray3d.h"
+#include "util/image.h"
+
+class Camera {
+    size_t image_w = 1280, image_h = 720;
+    double viewport_w = 0, viewport_h = 0;
+    Vec3D pixel_delta_x, pixel_delta_y;
+    Ray3D camera{.origin = Point3D{0, 0, 0}, .dir = Vec3D{0, 0, -1}};
+    std::optional<Point3D> camera_lookat;
+    Vec3D view_up_dir{0, 1, 0};
+    Vec3D cam_basis_x, cam_basis_y, cam_basis_z;
+    std::optional<double> focus_dist;
+    double defocus_angle = 0;
+    Vec3D defocus_disk_x, defocus_disk_y;
+    Point3D pixel00_loc;
+    size_t samples_per_pixel = 1;
+    size_t max_depth = 10;
+    std::optional<double> vertical_fov{90}, horizontal_fov;
+    RGB background{RGB::from_mag(0.5)};
+    crt_camera_settings settings{};
+    crt_camera resolved{};
+
+    static Vec3D v(const double* p) { return Vec3D{p[0], p[1], p[2]}; }
+    static void put(double* p, const Vec3D& a) { p[0] = a.x; p[1] = a.y; p[2] = a.z; }
+
+    // Camera::init (camera.h:87-157), computed by crt_camera_resolve; the same state updates
+    // (direction from the lookat point, default focus distance) are kept here.
+    void init() {
+        if (camera_lookat) camera.dir = *camera_lookat - camera.origin;
+        if (!focus_dist) focus_dist = camera.dir.mag();
+        crt_camera_settings s{};
+        s.image_w = static_cast<uint32_t>(image_w);
+        s.image_h = static_cast<uint32_t>(image_h);
+        s.samples_per_pixel = static_cast<uint32_t>(samples_per_pixel);
+        s.max_depth = static_cast<uint32_t>(max_depth);
+        put(s.center, camera.origin);
+        put(s.direction, camera.dir);
+        put(s.up, view_up_dir);
+        s.has_focus_dist = 1;
+        s.focus_dist = *focus_dist;
+        s.fov_is_vertical = vertical_fov.has_value();
+        s.fov = vertical_fov ? *vertical_fov : *horizontal_fov;
+        s.defocus_angle = defocus_angle;
+        s.background[0] = background.r;
+        s.background[1] = background.g;
+        s.background[2] = background.b;
+        if (crt_camera_resolve(&s, &resolved)) crt_api::die("crt_camera_resolve");
+        settings = s;
+        const double aspect = static_cast<double>(image_w) / static_cast<double>(image_h);
+        if (vertical_fov) {
+            viewport_h = 2 * *focus_dist * std::tan(*vertical_fov / 2);
+            viewport_w = viewport_h * aspect;
+        } else {
+            viewport_w = 2 * *focus_dist * std::tan(*horizontal_fov / 2);
+            viewport_h = viewport_w / aspect;
+        }
+        cam_basis_z = -camera.dir.unit_vector();
+        cam_basis_x = cross(view_up_dir, cam_basis_z).unit_vector();
+        cam_basis_y = cross(cam_basis_z, cam_basis_x);
+        pixel_delta_x = v(resolved.pixel_delta_x);
+        pixel_delta_y = v(resolved.pixel_delta_y);
+        pixel00_loc = v(resolved.pixel00);
+        defocus_disk_x = v(resolved.defocus_disk_x);
+        defocus_disk_y = v(resolved.defocus_disk_y);
+    }
+
+    // CRT_DUMP_SCENE=<file>: write the flattened world + camera as a CRTS file (the format of
+    // cpp_raytracer_amd.SceneData) and exit instead of rendering (scene-provenance tests)
+    void dump_and_exit(const crt_api::GpuScene& g, const char* path) {
+        std::FILE* f = std::fopen(path, "wb");
+        if (!f) crt_api::die(std::string("cannot open ") + path);
+        const uint32_t ver = 1;
+        const uint64_t nm = g.material_records.size(), no = g.object_records.size();
+        std::fwrite("CRTS", 1, 4, f);
+        std::fwrite(&ver, 4, 1, f);
+        std::fwrite(&nm, 8, 1, f);
+        std::fwrite(&no, 8, 1, f);
+        std::fwrite(&settings, sizeof settings, 1, f);
+        std::fwrite(g.material_records.data(), sizeof(crt_material), nm, f);
+        std::fwrite(g.object_records.data(), sizeof(crt_object), no, f);
+        std::fclose(f);
+        std::exit(0);
+    }
+
+    Image render_scene(const crt_api::GpuScene& g) {
+        crt_scene* scene = g.get();
+        init();
+        if (const char* dump = std::getenv("CRT_DUMP_SCENE")) dump_and_exit(g, dump);
+        resolved.base_seed = SeedSeqGenerator::get_instance().next_seed();
+        int devices = 0;
+        if (crt_device_count(&devices) || devices == 0) crt_api::die("Camera::render");
+        if (const char* e = std::getenv("CRT_NUM_DEVICES")) devices = std::max(1, std::min(devices, std::atoi(e)));
+        std::cout << "Rendering " << image_w << " x " << image_h << " image (" << samples_per_pixel
+                  << " spp) on " << devices << " GPU" << (devices > 1 ? "s" : "") << std::endl;
+        std::vector<double> rgb(image_w * image_h * 3);
+        crt_render_stats stats{};
+        auto t0 = std::chrono::steady_clock::now();
+        if (crt_render(scene, &resolved, devices, rgb.data(), &stats)) crt_api::die("Camera::render");
+        auto ms = ms_diff(t0, std::chrono::steady_clock::now());
+        std::cout << "Rendering " << image_w << " x " << image_h << " image: Finished in " << ms << "ms\n"
+                  << std::endl;
+        auto img = Image::with_dimensions(image_w, image_h);
+        for (size_t r = 0; r < image_h; ++r)
+            for (size_t c = 0; c < image_w; ++c) {
+                const double* p = &rgb[(r * image_w + c) * 3];
+                img[r][c] = RGB::from_mag(p[0], p[1], p[2]);
+            }
+        return img;
+    }
+
+public:
+    // camera.h:264-297: a BVH renders through its own node arrays; any other Hittable renders
+    // with the semantics of its own hit_by (one always-entered leaf in object order)
+    template <typename T>
+    requires std::is_base_of_v<Hittable, T>
+    Image render(const T& world) {
+        if constexpr (std::is_same_v<T, BVH>) {
+            return render_scene(world.gpu_scene());
+        } else {
+            crt_api::GpuScene s(world, 32, 12, true);
+            return render_scene(s);
+        }
+    }
+
+    // camera.h:301-303: a Scene renders through BVH(world)
+    Image render(const Scene& world) { return render(BVH(world)); }
+
+    Camera& set_camera_center(const Point3D& p) { camera.origin = p; return *this; }
+    Camera& set_camera_direction(const Vec3D& d) { camera.dir = d; return *this; }
+    Camera& set_camera_direction_towards(const Point3D& p) {
+        camera.dir = p - camera.origin;
+        camera_lookat.reset();
+        return *this;
+    }
+    Camera& set_camera_lookat(const Point3D& p) { camera_lookat = p; return *this; }
+    Camera& set_focus_distance(double d) { focus_dist = d; return *this; }
+    Camera& set_defocus_angle(double deg) { defocus_angle = deg * std::numbers::pi / 180; return *this; }
+    Camera& turn_blur_off() { defocus_angle = 0; return *this; }
+    Camera& set_camera_up_direction(const Vec3D& d) { view_up_dir = d; return *this; }
+    Camera& set_image_width(size_t w) { image_w = w; return *this; }
+    Camera& set_image_height(size_t h) { image_h = h; return *this; }
+    Camera& set_image_dimensions(size_t w, size_t h) { image_w = w; image_h = h; return *this; }
+    Camera& set_image_by_width_and_aspect_ratio(size_t w, double aspect) {
+        auto h = static_cast<size_t>(std::round(static_cast<double>(w) / aspect));
+        return set_image_dimensions(w, std::max(size_t{1}, h));
+    }
+    Camera& set_image_by_height_and_aspect_ratio(size_t h, double aspect) {
+        auto w = static_cast<size_t>(std::round(static_cast<double>(h) * aspect));
+        return set_image_dimensions(std::max(size_t{1}, w), h);
+    }
+    Camera& set_samples_per_pixel(size_t s) { samples_per_pixel = s; return *this; }
+    Camera& set_max_depth(size_t d) { max_depth = d; return *this; }
+    Camera& set_vertical_fov(double deg) {
+        vertical_fov = deg * std::numbers::pi / 180;
+        horizontal_fov.reset();
+        return *this;
+    }
+    Camera& set_horizontal_fov(double deg) {
+        horizontal_fov = deg * std::numbers::pi / 180;
+        vertical_fov.reset();
+        return *this;
+    }
+    Camera& set_background(const RGB& c) { background = c; return *this; }
+
+    void print_to(std::ostream& os) {
+        init();
+        os << "Camera {\n"
+           << "\tImage dimensions: " << image_w << " x " << image_h << '\n'
+           << "\tViewport dimensions: " << viewport_w << " x " << viewport_h << '\n'
+           << "\tpixel_delta_x: " << pixel_delta_x << '\n'
+           << "\tpixel_delta_y: " << pixel_delta_y << '\n'
+           << "\tCamera center: " << camera.origin << '\n'
+           << "\tCamera direction: " << camera.dir << '\n'
+           << "\tUp direction: " << view_up_dir << '\n'
+           << "\tCamera orientation x-, y-, and z- orthonormal basis vectors {"
+           << "\n\t\tx: " << cam_basis_x << "\n\t\ty: " << cam_basis_y << "\n\t\tz: " << cam_basis_z << "\n\t}\n"
+           << "\tFocus distance: " << *focus_dist << '\n'
+           << "\tDefocus angle: " << defocus_angle << " rad, " << defocus_angle * 180 / std::numbers::pi
+           << " degrees\n"
+           << "\tDefocus dist x-, y- orthonormal basis vectors {"
+           << "\n\t\tx: " << defocus_disk_x << "\n\t\ty: " << defocus_disk_y << "\n\t}\n"
+           << "\tTop-left pixel's center on viewport: " << pixel00_loc << '\n'
+           << "\tSamples per pixel: " << samples_per_pixel << '\n'
+           << "\tMaximum bounces per ray: " << max_depth << '\n'
+           << "\tVertical FOV (-1 means not given): " << vertical_fov.value_or(-1) << " rad, "
+           << (vertical_fov ? *vertical_fov * 180 / std::numbers::pi : -1) << " degrees\n"
+           << "\tHorizontal FOV (-1 means not given): " << horizontal_fov.value_or(-1) << " rad, "
+           << (horizontal_fov ? *horizontal_fov * 180 / std::numbers::pi : -1) << " degrees\n}";
+    }
+};
+
+inline std::ostream& operator<<(std::ostream& os, Camera cam) {
+    cam.print_to(os);
+    return os;
+}
+
+#endif
