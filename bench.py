@@ -94,6 +94,7 @@ def main():
     import torch.distributed as dist
     import cpp_raytracer_amd as crt
     from cpp_raytracer_amd import Tiling, camera_with
+    from cpp_raytracer_amd.tiles import TileGather, owned_rows
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -120,15 +121,12 @@ def main():
     h, w = args.height, args.width
     rb = 16
     tiling = Tiling(rb, world, rank, 0)
-    owned = [r for r in range(h) if (r // rb) % world == rank]
-    max_owned = max(sum(1 for r in range(h) if (r // rb) % world == k) for k in range(world))
+    owned = owned_rows(h, rb, world, rank)
     log(f"scene {args.scene}: {info.num_primitives} prims, {info.num_nodes} nodes, depth {info.depth}, "
         f"BVH build {info.build_ms:.1f} ms, setup {time.time() - t0:.1f} s")
 
     frame = torch.zeros(h, w, 3, dtype=torch.float64, device="cuda")
-    owned_idx = torch.tensor(owned, dtype=torch.long, device="cuda")
-    tile = torch.zeros(max_owned, w, 3, dtype=torch.float64, device="cuda")
-    gathered = torch.zeros(world * max_owned, w, 3, dtype=torch.float64, device="cuda") if distributed else None
+    gather = TileGather(h, w, world, rank, "cuda", row_block=rb)
     stream = torch.cuda.current_stream()
 
     def step(ev=None):
@@ -137,9 +135,8 @@ def main():
         scene.render_async(local, cam, frame.data_ptr(), stream.cuda_stream, tiling)
         if ev is not None:
             ev[1].record(stream)
-        if distributed:  # gather the row tiles (RCCL all-gather over xGMI)
-            tile[: len(owned)].copy_(frame.index_select(0, owned_idx))
-            dist.all_gather_into_tensor(gathered, tile)
+        if distributed:  # assemble the frame from every rank's row tiles (RCCL over xGMI)
+            gather.gather(frame)
 
     for _ in range(args.warmup):
         step()

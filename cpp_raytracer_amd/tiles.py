@@ -1,0 +1,54 @@
+"""Row-tile partition of a frame over ranks and the tile gather (RCCL over xGMI on MI355X; any
+torch.distributed backend works, gloo in the CPU tests).
+
+Rows are dealt in blocks of `row_block` (default 16): row r belongs to rank (r // row_block) %
+world. Interleaving balances the >10x per-row cost variance of real scenes (the sky rows of
+RTOW cost almost nothing). Every rank renders only its rows (crt_render_async with
+crt_tiling{row_block, world, rank}); the frame is then assembled from equal-size padded tiles with
+one all-gather. Because the RNG is per (pixel, sample) and the sample-chunk grouping depends only on
+spp, the assembled frame is bit-identical for any number of ranks.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+
+def owned_rows(height: int, row_block: int, world: int, rank: int) -> list[int]:
+    """The rows rank `rank` renders (crt_tiling semantics of include/crt_render.h)."""
+    return [r for r in range(height) if (r // row_block) % world == rank]
+
+
+class TileGather:
+    """Gathers every rank's rows of a (h, w, 3) frame into a full frame on every rank."""
+
+    def __init__(self, height: int, width: int, world: int, rank: int, device, row_block: int = 16,
+                 dtype=torch.float64, group=None):
+        self.h, self.w, self.world, self.rank, self.group = height, width, world, rank, group
+        rows = [owned_rows(height, row_block, world, k) for k in range(world)]
+        self.max_rows = max(len(r) for r in rows)
+        self.mine = torch.tensor(rows[rank], dtype=torch.long, device=device)
+        self.n_mine = len(rows[rank])
+        # where each gathered tile row lands in the frame (padding rows are dropped)
+        dst, src = [], []
+        for k, rk in enumerate(rows):
+            for i, r in enumerate(rk):
+                dst.append(r)
+                src.append(k * self.max_rows + i)
+        self.dst = torch.tensor(dst, dtype=torch.long, device=device)
+        self.src = torch.tensor(src, dtype=torch.long, device=device)
+        self.tile = torch.zeros(self.max_rows, width, 3, dtype=dtype, device=device)
+        self.parts = [torch.zeros_like(self.tile) for _ in range(world)]
+        self.full = torch.zeros(world * self.max_rows, width, 3, dtype=dtype, device=device)
+
+    def gather(self, frame: torch.Tensor) -> torch.Tensor:
+        """frame: this rank's (h, w, 3) buffer with its own rows rendered. Returns the assembled
+        frame (a new tensor on every rank)."""
+        if self.world == 1:
+            return frame
+        self.tile[: self.n_mine].copy_(frame.index_select(0, self.mine))
+        dist.all_gather(self.parts, self.tile, group=self.group)
+        torch.cat(self.parts, out=self.full)
+        out = torch.empty_like(frame)
+        out.index_copy_(0, self.dst, self.full.index_select(0, self.src))
+        return out
