@@ -47,7 +47,7 @@ def parse():
     ap.add_argument("--spp", type=int, default=500)
     ap.add_argument("--depth", type=int, default=50)
     ap.add_argument("--base-seed", type=int, default=2024)
-    ap.add_argument("--cpu-spp", type=int, default=40, help="spp of the bounded CPU-baseline sample")
+    ap.add_argument("--cpu-spp", type=int, default=500, help="spp of the CPU-baseline sample (500 = the full frame)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, host cores)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pmc-json", default=str(ROOT / "profiles" / "pmc_latest.json"))
