@@ -80,7 +80,9 @@ class RenderStats(C.Structure):
     _fields_ = [("samples", C.c_uint64), ("rays", C.c_uint64), ("nodes_visited", C.c_uint64),
                 ("sphere_tests", C.c_uint64), ("parallelogram_tests", C.c_uint64),
                 ("kernel_ms", C.c_double), ("ticks_walk", C.c_uint64), ("ticks_leaf", C.c_uint64),
-                ("ticks_shade", C.c_uint64), ("ticks_total", C.c_uint64)]
+                ("ticks_shade", C.c_uint64), ("ticks_total", C.c_uint64),
+                ("wave_iters_walk", C.c_uint64), ("wave_iters_leaf", C.c_uint64),
+                ("wave_iters_shade", C.c_uint64)]
 
 
 # numpy views of the same records (for bulk scene I/O)

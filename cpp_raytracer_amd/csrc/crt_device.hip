@@ -31,7 +31,10 @@ namespace crt {
 
 namespace dev {
 
-constexpr int kBlock = 256;          // 4 waves; each wave owns one 8x8 pixel tile
+#ifndef CRT_BLOCK
+#define CRT_BLOCK 256
+#endif
+constexpr int kBlock = CRT_BLOCK;     // waves of 64; each wave starts on one 8x8 pixel tile
 constexpr double kScale = 1 / static_cast<double>(4294967295u - 1);  // rand_util.h:110-112
 
 struct SceneView {
@@ -67,7 +70,14 @@ struct Work {
 struct Counters {
     unsigned long long rays, nodes, sphere_tests, quad_tests;
     unsigned long long cyc_walk, cyc_leaf, cyc_shade, cyc_total;  // wave cycles (instrumented pass)
+    unsigned long long it_walk, it_leaf, it_shade;  // wave iterations (lane utilization)
 };
+
+// counts one per wave: only the lowest active lane increments
+__device__ __forceinline__ bool wave_leader() {
+    const uint64_t m = __ballot(1);
+    return (threadIdx.x & 63) == static_cast<uint32_t>(__ffsll(static_cast<long long>(m)) - 1);
+}
 
 // ---- reference RNG (rand_util.h:85-117) with per-sample state ------------------------------
 __device__ __forceinline__ double rnd(uint32_t& s, double lo, double hi) {
@@ -370,7 +380,10 @@ __device__ __forceinline__ void walk_step(const SceneView& S, Stack<SE>& st, con
     const double bz0 = b[4 + nz], bz1 = b[5 - nz];
     const uint4 meta = reinterpret_cast<const uint4*>(S.nodes + cur)[3];  // index count axis flags
     const uint32_t top = st.get(sp > 0 ? static_cast<int>(sp) - 1 : 0);  // speculative pop
-    if (COUNT) ctr.nodes++;
+    if (COUNT) {
+        ctr.nodes++;
+        if (wave_leader()) ctr.it_walk++;
+    }
     double xtmin = (bx0 - o[0]) * R.inv[0];
     double xtmax = (bx1 - o[0]) * R.inv[0];
     const double ytmin = (by0 - o[1]) * R.inv[1];
@@ -409,7 +422,10 @@ __device__ __forceinline__ void leaf_step(const SceneView& S, Stack<SE>& st, con
         DevSphere cur = S.spheres[R.first];
         for (uint32_t i = R.first; i < end; ++i) {
             const DevSphere nxt = S.spheres[i + 1 < end ? i + 1 : i];
-            if (COUNT) ctr.sphere_tests++;
+            if (COUNT) {
+                ctr.sphere_tests++;
+                if (wave_leader()) ctr.it_leaf++;
+            }
             double t;
             if (hit_sphere(cur, o, d, R.a, tmin, R.tmax, t)) {
                 R.tmax = t;
@@ -423,6 +439,7 @@ __device__ __forceinline__ void leaf_step(const SceneView& S, Stack<SE>& st, con
             const uint32_t ref = S.refs[i];
             double t;
             bool h;
+            if (COUNT && wave_leader()) ctr.it_leaf++;
             if (ref & kRefQuad) {
                 if (COUNT) ctr.quad_tests++;
                 h = hit_quad(S.quads[ref & ~kRefQuad], o, d, tmin, R.tmax, t);
@@ -691,6 +708,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRT_WAVE
 #endif
             if (COUNT) cs -= wall_clock64();
             if (R.state == kDone) {
+                if (COUNT && wave_leader()) ctr.it_shade++;
                 bool ended = shade(S, C, P, R.found, R.ref, R.tmax, acc);
                 // a scattered ray with no bounce left returns RGB::zero() (camera.h:211-213)
                 if (!ended && P.depth == 0) ended = true;
@@ -729,6 +747,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRT_WAVE
             atomicAdd(&counters->cyc_shade, ctr.cyc_shade);
             atomicAdd(&counters->cyc_total, wall_clock64() - t_start);
         }
+        // iteration counters are incremented by whichever lane led that iteration
+        atomicAdd(&counters->it_walk, ctr.it_walk);
+        atomicAdd(&counters->it_leaf, ctr.it_leaf);
+        atomicAdd(&counters->it_shade, ctr.it_shade);
     }
 }
 
@@ -993,6 +1015,9 @@ static int launch_render(const crt_scene* s, int device, const crt_camera* cam, 
         count_stats->ticks_leaf = h.cyc_leaf;
         count_stats->ticks_shade = h.cyc_shade;
         count_stats->ticks_total = h.cyc_total;
+        count_stats->wave_iters_walk = h.it_walk;
+        count_stats->wave_iters_leaf = h.it_leaf;
+        count_stats->wave_iters_shade = h.it_shade;
     }
     return CRT_OK;
 }

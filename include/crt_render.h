@@ -163,6 +163,9 @@ typedef struct crt_render_stats {
     /* wave-time breakdown of the instrumented pass (sum over waves, 100 MHz ticks): interior
      * BVH walk, leaf primitive tests, shading + path regeneration, whole wave lifetime */
     uint64_t ticks_walk, ticks_leaf, ticks_shade, ticks_total;
+    /* wave iterations of each phase: lane utilization = lane work / (iterations * 64) with lane
+     * work = nodes_visited, sphere+parallelogram tests, rays respectively */
+    uint64_t wave_iters_walk, wave_iters_leaf, wave_iters_shade;
 } crt_render_stats;
 
 /* ---- entry points ---------------------------------------------------------------------- */
