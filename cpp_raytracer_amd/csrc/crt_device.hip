@@ -65,6 +65,7 @@ struct Work {
     uint32_t lds_nodes, lds_refs, lds_spheres, lds_quads, lds_stack;
     uint32_t bytes_nodes, bytes_refs, bytes_spheres, bytes_quads;
     uint32_t sphere_only;   // every primitive is a sphere: refs[slot] == slot
+    uint32_t exact_slab;    // the scene needs walk_step's EXACT variant for every ray
 };
 
 struct Counters {
@@ -338,18 +339,22 @@ __device__ __forceinline__ bool trace(const SceneView& S, Stack<SE>& st, const d
 // reference's BVH::hit_by.
 enum : uint32_t { kWalk = 0, kLeaf = 1, kDone = 2, kIdle = 3 };
 
+constexpr uint32_t kZeroDir = 8u;
+
 struct Trav {
     double inv[3];
     double a;        // dot(d, d)
     double tmax;
     uint32_t cur, sp, ref;
-    uint32_t first, count;  // pending leaf
-    uint32_t neg;    // bit k: d[k] < 0
+    uint32_t neg;    // bit k: d[k] < 0; kZeroDir: a slab value may be NaN (walk_step EXACT)
     uint32_t state;
     bool found;
 };
 
-__device__ __forceinline__ void trav_init(const double d[3], Trav& R) {
+__device__ __forceinline__ bool finite_nonzero(double x) { return fabs(x) < __builtin_inf() && x != 0; }
+__device__ __forceinline__ bool finite(double x) { return fabs(x) < __builtin_inf(); }
+
+__device__ __forceinline__ void trav_init(const double o[3], const double d[3], Trav& R) {
     R.inv[0] = 1 / d[0];
     R.inv[1] = 1 / d[1];
     R.inv[2] = 1 / d[2];
@@ -358,56 +363,78 @@ __device__ __forceinline__ void trav_init(const double d[3], Trav& R) {
     R.cur = 0;
     R.sp = 0;
     R.ref = 0;
-    R.first = 0;
-    R.count = 0;
-    R.neg = (d[0] < 0 ? 1u : 0u) | (d[1] < 0 ? 2u : 0u) | (d[2] < 0 ? 4u : 0u);
+    const bool fast = finite_nonzero(R.inv[0]) && finite_nonzero(R.inv[1]) && finite_nonzero(R.inv[2]) &&
+                      finite(o[0]) && finite(o[1]) && finite(o[2]);
+    R.neg = (d[0] < 0 ? 1u : 0u) | (d[1] < 0 ? 2u : 0u) | (d[2] < 0 ? 4u : 0u) | (fast ? 0u : kZeroDir);
     R.state = kWalk;
     R.found = false;
 }
 
 // one node of the DFS (bvh.h:617-712 loop body without the leaf's primitive loop), branch-free:
-// the node's bounds are loaded by per-lane address (x[neg] / x[!neg] of aabb.h:141-159), its
-// index/count/axis/flags and the stack top are loaded in the same batch, and the push / pop /
-// leaf / done outcomes are selected rather than branched to (only the push is a masked store).
-template <typename SE, bool COUNT>
+// the node's bounds, index/count/axis/flags and the stack top are loaded in one batch, and the
+// push / pop / leaf / done outcomes are selected rather than branched to (only the push is a
+// masked store).
+// Slab test (aabb.h:141-159). The reference swaps each axis' (t0, t1) by the sign of d and then
+// narrows with "if (y > x) x = y"-style selects; for NaN-free slab values that is exactly
+//   near_k = min(t0_k, t1_k), far_k = max(t0_k, t1_k),
+//   enter  = max(near) <= min(far)  &&  max(near) < tmax  &&  min(far) > tmin
+// (c1 && c2 of the reference <=> every near_i <= far_j; +-0 ties only meet comparisons). A slab
+// value is NaN only for 0 * inf or inf - inf: rays whose inv[] is not finite and nonzero or whose
+// origin is not finite (R.neg & kZeroDir), and scenes with an inverted / NaN node box
+// (Work::exact_slab, where min/max would reorder the axis) take the EXACT variant, the reference's select sequence verbatim
+// with per-lane bound addresses x[neg] / x[!neg].
+template <typename SE, bool COUNT, bool EXACT>
 __device__ __forceinline__ void walk_step(const SceneView& S, Stack<SE>& st, const double o[3],
                                           double tmin, Trav& R, Counters& ctr) {
     const uint32_t cur = R.cur, sp = R.sp;
-    const double* b = reinterpret_cast<const double*>(S.nodes + cur);
-    const uint32_t nx = R.neg & 1u, ny = (R.neg >> 1) & 1u, nz = (R.neg >> 2) & 1u;
-    const double bx0 = b[0 + nx], bx1 = b[1 - nx];
-    const double by0 = b[2 + ny], by1 = b[3 - ny];
-    const double bz0 = b[4 + nz], bz1 = b[5 - nz];
     const uint4 meta = reinterpret_cast<const uint4*>(S.nodes + cur)[3];  // index count axis flags
     const uint32_t top = st.get(sp > 0 ? static_cast<int>(sp) - 1 : 0);  // speculative pop
     if (COUNT) {
         ctr.nodes++;
         if (wave_leader()) ctr.it_walk++;
     }
-    double xtmin = (bx0 - o[0]) * R.inv[0];
-    double xtmax = (bx1 - o[0]) * R.inv[0];
-    const double ytmin = (by0 - o[1]) * R.inv[1];
-    const double ytmax = (by1 - o[1]) * R.inv[1];
-    const double ztmin = (bz0 - o[2]) * R.inv[2];
-    const double ztmax = (bz1 - o[2]) * R.inv[2];
-    const bool c1 = !(xtmin > ytmax || ytmin > xtmax);
-    if (ytmin > xtmin) xtmin = ytmin;
-    if (ytmax < xtmax) xtmax = ytmax;
-    const bool c2 = !(xtmin > ztmax || ztmin > xtmax);
-    if (ztmin > xtmin) xtmin = ztmin;
-    if (ztmax < xtmax) xtmax = ztmax;
-    const bool enter = (c1 & c2 & (xtmin < R.tmax) & (xtmax > tmin)) |
-                       ((meta.w & kNodeAlways) != 0);
-    const bool leaf = enter && meta.y > 0;
+    bool enter;
+    if (!EXACT) {
+        const double2* b = reinterpret_cast<const double2*>(S.nodes + cur);
+        const double2 bx = b[0], by = b[1], bz = b[2];
+        const double x0 = (bx.x - o[0]) * R.inv[0], x1 = (bx.y - o[0]) * R.inv[0];
+        const double y0 = (by.x - o[1]) * R.inv[1], y1 = (by.y - o[1]) * R.inv[1];
+        const double z0 = (bz.x - o[2]) * R.inv[2], z1 = (bz.y - o[2]) * R.inv[2];
+        const double near = fmax(fmax(fmin(x0, x1), fmin(y0, y1)), fmin(z0, z1));
+        const double far = fmin(fmin(fmax(x0, x1), fmax(y0, y1)), fmax(z0, z1));
+        enter = ((near <= far) & (near < R.tmax) & (far > tmin)) | ((meta.w & kNodeAlways) != 0);
+    } else {
+        const double* b = reinterpret_cast<const double*>(S.nodes + cur);
+        const uint32_t nx = R.neg & 1u, ny = (R.neg >> 1) & 1u, nz = (R.neg >> 2) & 1u;
+        const double bx0 = b[0 + nx], bx1 = b[1 - nx];
+        const double by0 = b[2 + ny], by1 = b[3 - ny];
+        const double bz0 = b[4 + nz], bz1 = b[5 - nz];
+        double xtmin = (bx0 - o[0]) * R.inv[0];
+        double xtmax = (bx1 - o[0]) * R.inv[0];
+        const double ytmin = (by0 - o[1]) * R.inv[1];
+        const double ytmax = (by1 - o[1]) * R.inv[1];
+        const double ztmin = (bz0 - o[2]) * R.inv[2];
+        const double ztmax = (bz1 - o[2]) * R.inv[2];
+        const bool c1 = !(xtmin > ytmax || ytmin > xtmax);
+        if (ytmin > xtmin) xtmin = ytmin;
+        if (ytmax < xtmax) xtmax = ytmax;
+        const bool c2 = !(xtmin > ztmax || ztmin > xtmax);
+        if (ztmin > xtmin) xtmin = ztmin;
+        if (ztmax < xtmax) xtmax = ztmax;
+        enter = (c1 & c2 & (xtmin < R.tmax) & (xtmax > tmin)) | ((meta.w & kNodeAlways) != 0);
+    }
+    // inner: descend to the near child, push the far one; leaf: stay on the node (leaf_step
+    // reads its primitive range); missed: pop, or done on an empty stack (sp is then dead).
+    // The far child is stored at level sp whatever the outcome (level sp is above the live
+    // stack unless it is pushed; the stack has depth + 1 levels), keeping the step branch-free.
     const bool inner = enter && meta.y == 0;
     const bool far_first = (R.neg >> meta.z) & 1u;
-    if (inner) st.put(static_cast<int>(sp), far_first ? cur + 1 : meta.x);
-    const bool pop = !enter && sp > 0;
-    R.cur = inner ? (far_first ? meta.x : cur + 1) : (pop ? top : cur);
-    R.sp = inner ? sp + 1 : (pop ? sp - 1 : sp);
-    R.first = leaf ? meta.x : R.first;
-    R.count = leaf ? meta.y : R.count;
-    R.state = leaf ? kLeaf : ((!enter && sp == 0) ? kDone : kWalk);
+    const uint32_t near_child = far_first ? meta.x : cur + 1;
+    const uint32_t far_child = far_first ? cur + 1 : meta.x;
+    st.put(static_cast<int>(sp), far_child);
+    R.cur = inner ? near_child : (enter ? cur : top);
+    R.sp = inner ? sp + 1 : (enter ? sp : sp - 1);
+    R.state = enter ? (meta.y ? kLeaf : kWalk) : (sp ? kWalk : kDone);
 }
 
 // the entered leaf's primitives in order (bvh.h:635-652), then "return" to the DFS.
@@ -417,10 +444,11 @@ template <typename SE, bool COUNT>
 __device__ __forceinline__ void leaf_step(const SceneView& S, Stack<SE>& st, const double o[3],
                                           const double d[3], double tmin, bool sphere_only,
                                           Trav& R, Counters& ctr) {
-    const uint32_t end = R.first + R.count;
+    const uint2 range = reinterpret_cast<const uint2*>(S.nodes + R.cur)[6];  // index, count
+    const uint32_t end = range.x + range.y;
     if (sphere_only) {
-        DevSphere cur = S.spheres[R.first];
-        for (uint32_t i = R.first; i < end; ++i) {
+        DevSphere cur = S.spheres[range.x];
+        for (uint32_t i = range.x; i < end; ++i) {
             const DevSphere nxt = S.spheres[i + 1 < end ? i + 1 : i];
             if (COUNT) {
                 ctr.sphere_tests++;
@@ -435,7 +463,7 @@ __device__ __forceinline__ void leaf_step(const SceneView& S, Stack<SE>& st, con
             cur = nxt;
         }
     } else {
-        for (uint32_t i = R.first; i < end; ++i) {
+        for (uint32_t i = range.x; i < end; ++i) {
             const uint32_t ref = S.refs[i];
             double t;
             bool h;
@@ -665,7 +693,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRT_WAVE
     // max_depth == 0: ray_color returns RGB::zero() for every sample (camera.h:211-213)
     if (valid && C.max_depth > 0 && s < s_end) {
         start_path(C, row, col, sample_seed(C.base_seed, pixel, s), P);
-        trav_init(P.d, R);
+        trav_init(P.o, P.d, R);
         if (COUNT) ctr.rays++;
     }
     unsigned long long cw = 0, cl = 0, cs = 0;
@@ -675,7 +703,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRT_WAVE
         // finished ray, or none is traversing
         while (true) {
             if (COUNT) cw -= wall_clock64();
-            while (R.state == kWalk) walk_step<SE, COUNT>(S, st, P.o, C.t_min, R, ctr);
+            if (!W.exact_slab && __ballot(R.state == kWalk && (R.neg & kZeroDir)) == 0) {
+                while (R.state == kWalk) walk_step<SE, COUNT, false>(S, st, P.o, C.t_min, R, ctr);
+            } else {
+                while (R.state == kWalk) walk_step<SE, COUNT, true>(S, st, P.o, C.t_min, R, ctr);
+            }
             if (COUNT) cw += wall_clock64();
             if (COUNT) cl -= wall_clock64();
             if (R.state == kLeaf) leaf_step<SE, COUNT>(S, st, P.o, P.d, C.t_min, W.sphere_only != 0, R, ctr);
@@ -690,7 +722,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRT_WAVE
 #else
         // walk: one BVH node for every walking lane
         if (COUNT) cw -= wall_clock64();
-        if (R.state == kWalk) walk_step<SE, COUNT>(S, st, P.o, C.t_min, R, ctr);
+        if (R.state == kWalk) walk_step<SE, COUNT, true>(S, st, P.o, C.t_min, R, ctr);
         if (COUNT) cw += wall_clock64();
         const uint64_t m_walk = __ballot(R.state == kWalk);
         const uint64_t m_leaf = __ballot(R.state == kLeaf);
@@ -717,7 +749,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRT_WAVE
                     else start_path(C, row, col, sample_seed(C.base_seed, pixel, s), P);
                 }
                 if (R.state != kIdle) {
-                    trav_init(P.d, R);
+                    trav_init(P.o, P.d, R);
                     if (COUNT) ctr.rays++;
                 }
             }
@@ -937,8 +969,11 @@ static uint32_t count_owned(uint32_t h, uint32_t rb, uint32_t tc, uint32_t ti) {
 
 static size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
 
-constexpr size_t kLdsSceneBudget = 40 * 1024;  // scene + stack; keeps >= 3 blocks (12 waves)/CU
-constexpr size_t kLdsStackBudget = 32 * 1024;
+#ifndef CRT_LDS_BUDGET_KB
+#define CRT_LDS_BUDGET_KB 40
+#endif
+constexpr size_t kLdsSceneBudget = CRT_LDS_BUDGET_KB * 1024;  // scene + stack per block
+constexpr size_t kLdsStackBudget = 32 * 1024 * (dev::kBlock / 256);
 
 template <typename SE, bool GSTACK, bool LSCENE>
 static int launch_render(const crt_scene* s, int device, const crt_camera* cam, const dev::Work& w0,
@@ -1027,7 +1062,8 @@ static int launch_render(const crt_scene* s, int device, const crt_camera* cam, 
 template <typename SE>
 static int dispatch_render(const crt_scene* s, int device, const crt_camera* cam, dev::Work W,
                            double* d_rgb, hipStream_t st, crt_render_stats* count_stats) {
-    const size_t stack_bytes = align16(static_cast<size_t>(std::max<uint32_t>(1, s->depth)) * dev::kBlock * sizeof(SE));
+    // depth + 1 levels: walk_step stores the far child at level sp unconditionally
+    const size_t stack_bytes = align16(static_cast<size_t>(s->depth + 1) * dev::kBlock * sizeof(SE));
     W.bytes_nodes = static_cast<uint32_t>(align16(s->dnodes.size() * sizeof(DevNode)));
     W.bytes_refs = static_cast<uint32_t>(align16(s->refs.size() * 4));
     W.bytes_spheres = static_cast<uint32_t>(align16(s->spheres.size() * sizeof(DevSphere)));
@@ -1089,6 +1125,7 @@ int device_render(const crt_scene* s, int device, const crt_camera* cam, const c
     W.tiles_y = (W.owned_rows + 7) / 8;
     W.tiles = W.tiles_x * W.tiles_y;
     W.sphere_only = (s->quads.empty() && !s->spheres.empty()) ? 1u : 0u;
+    W.exact_slab = (s->exact_slab || std::getenv("CRT_EXACT_SLAB") != nullptr) ? 1u : 0u;
     hipStream_t st = static_cast<hipStream_t>(stream);
     if (count_stats) HIP_TRY(hipStreamCreate(&st));
     int r;

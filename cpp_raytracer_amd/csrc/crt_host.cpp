@@ -351,9 +351,12 @@ static int build_bvh(crt_scene* s, const crt_bvh_params& prm) {
 // device-layout staging arrays
 static void stage(crt_scene* s) {
     s->dnodes.resize(s->nodes.size());
+    s->exact_slab = false;
     for (size_t i = 0; i < s->nodes.size(); ++i) {
         const crt_bvh_node& n = s->nodes[i];
         DevNode& d = s->dnodes[i];
+        for (int k = 0; k < 3; ++k)
+            if (!(n.bounds[2 * k] <= n.bounds[2 * k + 1]) && !(n.flags & kNodeAlways)) s->exact_slab = true;
         std::memcpy(d.b, n.bounds, sizeof d.b);
         d.index = n.index;
         d.count = n.count;

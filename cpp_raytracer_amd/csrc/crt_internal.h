@@ -97,6 +97,7 @@ struct crt_scene {
     uint32_t max_leaf = 0;
     double build_ms = 0;
     bool linear = false;
+    bool exact_slab = false;  // some node box is inverted / NaN on an axis: walk_step EXACT only
     crt::DeviceCopy dev[crt::kMaxDevices];
     std::mutex mu;
 };

@@ -106,3 +106,18 @@ def test_baseline_config2_properties(crt):
     assert np.isfinite(an).all() and an.min() >= 0 and an.max() <= 1
     want = orc.render(d, 2024, threads=16, crop=(396, 404, 596, 604))
     check(an[396:404, 596:604], want)
+
+
+@pytest.mark.parametrize("name,seed,kw", [
+    ("rtow_final", 42, dict(image_w=120, image_h=80, samples_per_pixel=8)),
+    ("cornell", None, dict(image_w=64, image_h=64, samples_per_pixel=8, max_depth=100)),
+    ("christmas_tree", None, dict(image_w=96, image_h=54, samples_per_pixel=4)),
+])
+def test_minmax_slab_equals_reference_selects(crt, monkeypatch, name, seed, kw):
+    """walk_step's min/max slab (NaN-free rays) against its EXACT variant (the reference's
+    select sequence, forced for every ray by CRT_EXACT_SLAB): bit-identical frames."""
+    d = scene(crt, name, seed, **kw)
+    fast = gpu(crt, d, 40)
+    monkeypatch.setenv("CRT_EXACT_SLAB", "1")
+    exact = gpu(crt, d, 40)
+    assert np.array_equal(fast, exact)
