@@ -167,29 +167,65 @@ __device__ __forceinline__ bool slab(const NodeRegs& n, const double o[3], const
     return c1 & c2 & (xtmin < tmax) & (xtmax > tmin);
 }
 
+// sqrt(x) bit for bit for x in [2^-767, inf), given r = v_rsq_f64(x): hipcc's own gfx950
+// expansion of the IEEE sqrt (Goldschmidt + two Newton corrections) without its small-x scaling
+// and 0/inf fix-up, which are identities there. Outside that range: sqrt() itself.
+__device__ __forceinline__ double sqrt_from_rsq(double x, double r) {
+    if (__builtin_expect(!(x >= 0x1p-767 && x < __builtin_inf()), 0)) return sqrt(x);
+    double g = x * r, h = r * 0.5;
+    const double e = fma(-h, g, 0.5);
+    g = fma(g, e, g);
+    h = fma(h, e, h);
+    double d = fma(-g, g, x);
+    g = fma(d, h, g);
+    d = fma(-g, g, x);
+    return fma(d, h, g);
+}
+
+// Reciprocal of a ray's dot(d, d) for div_a: ia = RN(1 / a), or NaN when a is outside the range
+// where div_a's corrections are exact (then div_a divides).
+__device__ __forceinline__ double recip_a(double a) {
+    return (a >= 0x1p-500 && a <= 0x1p500) ? 1 / a : __builtin_nan("");
+}
+
+// n / a correctly rounded from ia = RN(1/a): q0 = n * ia, then two residual corrections
+// q += fma(-a, q, n) * ia (Markstein's theorem: with ia = RN(1/a) and q within 1 ulp, the
+// corrected q is RN(n / a); the first correction makes q faithful). No over/underflow for
+// |n|, a in [2^-500, 2^500]; anything else divides.
+__device__ __forceinline__ double div_a(double n, double a, double ia) {
+    const double an = fabs(n);
+    if (__builtin_expect(!(an >= 0x1p-500 && an <= 0x1p500 && ia == ia), 0)) return n / a;
+    double q = n * ia;
+    q = fma(fma(-a, q, n), ia, q);
+    return fma(fma(-a, q, n), ia, q);
+}
+
 // Sphere::hit_by (sphere.h:45-96) returning the accepted root through t.
 // Before the exact sqrt and divisions, a coarse bound (hardware rsq, error <= 2^-23 relative;
 // margins of 2^-12 on every term) proves "both roots >= t_max" or "both roots <= t_min" for
 // spheres that cannot be accepted; only those are skipped, so the accepted roots are exactly the
 // reference's. NaN/inf anywhere makes the bound inconclusive and falls through to the exact test.
+// The sqrt and the two divisions by a are the correctly rounded ones (sqrt_from_rsq, div_a with
+// ia = recip_a(a)).
 __device__ __forceinline__ bool hit_sphere(const DevSphere& sp, const double o[3], const double d[3],
-                                           double a, double tmin, double tmax, double& t) {
+                                           double a, double ia, double tmin, double tmax, double& t) {
     double ocx = o[0] - sp.c[0], ocy = o[1] - sp.c[1], ocz = o[2] - sp.c[2];
     double b = d[0] * ocx + d[1] * ocy + d[2] * ocz;
     double c = (ocx * ocx + ocy * ocy + ocz * ocz) - sp.r * sp.r;
     double disc = b * b - a * c;
     if (disc < 0) return false;
+    const double rs = __builtin_amdgcn_rsq(disc);
     {
-        const double sqa = disc * __builtin_amdgcn_rsq(disc);      // ~sqrt(disc)
+        const double sqa = disc * rs;                              // ~sqrt(disc)
         const double m = (fabs(b) + sqa) * 0x1p-12;                // covers every rounding error
         const bool beyond = (-b - sqa) - m > tmax * a * (1 + 0x1p-30);   // r1 > tmax, so r2 too
         const bool before = (-b + sqa) + m < tmin * a * (1 - 0x1p-30);   // r2 < tmin, so r1 too
         if (beyond || before) return false;
     }
-    double sq = sqrt(disc);
-    double root = (-b - sq) / a;
+    double sq = sqrt_from_rsq(disc, rs);
+    double root = div_a(-b - sq, a, ia);
     if (!(tmin < root && root < tmax)) {
-        root = (-b + sq) / a;
+        root = div_a(-b + sq, a, ia);
         if (!(tmin < root && root < tmax)) return false;
     }
     t = root;
@@ -277,6 +313,7 @@ __device__ __forceinline__ bool trace(const SceneView& S, Stack<SE>& st, const d
     const double inv[3] = {1 / d[0], 1 / d[1], 1 / d[2]};
     const uint32_t neg = (d[0] < 0 ? 1u : 0u) | (d[1] < 0 ? 2u : 0u) | (d[2] < 0 ? 4u : 0u);
     const double a = d[0] * d[0] + d[1] * d[1] + d[2] * d[2];  // dot(ray.dir, ray.dir)
+    const double ia = recip_a(a);
     bool found = false;
     int sp = 0;
     uint32_t cur = 0;
@@ -317,7 +354,7 @@ __device__ __forceinline__ bool trace(const SceneView& S, Stack<SE>& st, const d
                 h = hit_quad(S.quads[ref & ~kRefQuad], o, d, tmin, tmax, t);
             } else {
                 if (COUNT) ctr.sphere_tests++;
-                h = hit_sphere(S.spheres[ref], o, d, a, tmin, tmax, t);
+                h = hit_sphere(S.spheres[ref], o, d, a, ia, tmin, tmax, t);
             }
             if (h) {
                 tmax = t;
@@ -384,57 +421,66 @@ __device__ __forceinline__ void trav_init(const double o[3], const double d[3], 
 // (Work::exact_slab, where min/max would reorder the axis) take the EXACT variant, the reference's select sequence verbatim
 // with per-lane bound addresses x[neg] / x[!neg].
 template <typename SE, bool COUNT, bool EXACT>
-__device__ __forceinline__ void walk_step(const SceneView& S, Stack<SE>& st, const double o[3],
-                                          double tmin, Trav& R, Counters& ctr) {
-    const uint32_t cur = R.cur, sp = R.sp;
-    const uint4 meta = reinterpret_cast<const uint4*>(S.nodes + cur)[3];  // index count axis flags
-    const uint32_t top = st.get(sp > 0 ? static_cast<int>(sp) - 1 : 0);  // speculative pop
-    if (COUNT) {
-        ctr.nodes++;
-        if (wave_leader()) ctr.it_walk++;
+__device__ __forceinline__ void walk(const SceneView& S, Stack<SE>& st, const double o[3],
+                                     double tmin, Trav& R, Counters& ctr) {
+    uint32_t cur = R.cur, sp = R.sp;
+    while (true) {
+        const uint4 meta = reinterpret_cast<const uint4*>(S.nodes + cur)[3];  // index count axis flags
+        const uint32_t top = st.get(sp > 0 ? static_cast<int>(sp) - 1 : 0);  // speculative pop
+        if (COUNT) {
+            ctr.nodes++;
+            if (wave_leader()) ctr.it_walk++;
+        }
+        bool enter;
+        if (!EXACT) {
+            // linear-mode nodes (kNodeAlways) carry [-inf, inf] bounds in the device copy: with
+            // finite o and finite non-zero inv every slab is (-inf, inf), so they are entered
+            const double2* b = reinterpret_cast<const double2*>(S.nodes + cur);
+            const double2 bx = b[0], by = b[1], bz = b[2];
+            const double x0 = (bx.x - o[0]) * R.inv[0], x1 = (bx.y - o[0]) * R.inv[0];
+            const double y0 = (by.x - o[1]) * R.inv[1], y1 = (by.y - o[1]) * R.inv[1];
+            const double z0 = (bz.x - o[2]) * R.inv[2], z1 = (bz.y - o[2]) * R.inv[2];
+            const double near = fmax(fmax(fmin(x0, x1), fmin(y0, y1)), fmin(z0, z1));
+            const double far = fmin(fmin(fmax(x0, x1), fmax(y0, y1)), fmax(z0, z1));
+            enter = (near <= far) & (near < R.tmax) & (far > tmin);
+        } else {
+            const double* b = reinterpret_cast<const double*>(S.nodes + cur);
+            const uint32_t nx = R.neg & 1u, ny = (R.neg >> 1) & 1u, nz = (R.neg >> 2) & 1u;
+            const double bx0 = b[0 + nx], bx1 = b[1 - nx];
+            const double by0 = b[2 + ny], by1 = b[3 - ny];
+            const double bz0 = b[4 + nz], bz1 = b[5 - nz];
+            double xtmin = (bx0 - o[0]) * R.inv[0];
+            double xtmax = (bx1 - o[0]) * R.inv[0];
+            const double ytmin = (by0 - o[1]) * R.inv[1];
+            const double ytmax = (by1 - o[1]) * R.inv[1];
+            const double ztmin = (bz0 - o[2]) * R.inv[2];
+            const double ztmax = (bz1 - o[2]) * R.inv[2];
+            const bool c1 = !(xtmin > ytmax || ytmin > xtmax);
+            if (ytmin > xtmin) xtmin = ytmin;
+            if (ytmax < xtmax) xtmax = ytmax;
+            const bool c2 = !(xtmin > ztmax || ztmin > xtmax);
+            if (ztmin > xtmin) xtmin = ztmin;
+            if (ztmax < xtmax) xtmax = ztmax;
+            enter = (c1 & c2 & (xtmin < R.tmax) & (xtmax > tmin)) | ((meta.w & kNodeAlways) != 0);
+        }
+        // inner: descend to the near child, push the far one; missed: pop. The far child is
+        // stored at level sp whatever the outcome (level sp is above the live stack unless it is
+        // pushed; the stack has depth + 1 levels), so only the loop exit is a branch: on an
+        // entered leaf (cur stays on it; leaf_step reads its primitive range) or an empty stack.
+        const bool inner = enter && meta.y == 0;
+        const bool far_first = (R.neg >> meta.z) & 1u;
+        const uint32_t near_child = far_first ? meta.x : cur + 1;
+        const uint32_t far_child = far_first ? cur + 1 : meta.x;
+        st.put(static_cast<int>(sp), far_child);
+        if (!inner && (enter || sp == 0)) {
+            R.state = enter ? kLeaf : kDone;
+            break;
+        }
+        cur = inner ? near_child : top;
+        sp = inner ? sp + 1 : sp - 1;
     }
-    bool enter;
-    if (!EXACT) {
-        const double2* b = reinterpret_cast<const double2*>(S.nodes + cur);
-        const double2 bx = b[0], by = b[1], bz = b[2];
-        const double x0 = (bx.x - o[0]) * R.inv[0], x1 = (bx.y - o[0]) * R.inv[0];
-        const double y0 = (by.x - o[1]) * R.inv[1], y1 = (by.y - o[1]) * R.inv[1];
-        const double z0 = (bz.x - o[2]) * R.inv[2], z1 = (bz.y - o[2]) * R.inv[2];
-        const double near = fmax(fmax(fmin(x0, x1), fmin(y0, y1)), fmin(z0, z1));
-        const double far = fmin(fmin(fmax(x0, x1), fmax(y0, y1)), fmax(z0, z1));
-        enter = ((near <= far) & (near < R.tmax) & (far > tmin)) | ((meta.w & kNodeAlways) != 0);
-    } else {
-        const double* b = reinterpret_cast<const double*>(S.nodes + cur);
-        const uint32_t nx = R.neg & 1u, ny = (R.neg >> 1) & 1u, nz = (R.neg >> 2) & 1u;
-        const double bx0 = b[0 + nx], bx1 = b[1 - nx];
-        const double by0 = b[2 + ny], by1 = b[3 - ny];
-        const double bz0 = b[4 + nz], bz1 = b[5 - nz];
-        double xtmin = (bx0 - o[0]) * R.inv[0];
-        double xtmax = (bx1 - o[0]) * R.inv[0];
-        const double ytmin = (by0 - o[1]) * R.inv[1];
-        const double ytmax = (by1 - o[1]) * R.inv[1];
-        const double ztmin = (bz0 - o[2]) * R.inv[2];
-        const double ztmax = (bz1 - o[2]) * R.inv[2];
-        const bool c1 = !(xtmin > ytmax || ytmin > xtmax);
-        if (ytmin > xtmin) xtmin = ytmin;
-        if (ytmax < xtmax) xtmax = ytmax;
-        const bool c2 = !(xtmin > ztmax || ztmin > xtmax);
-        if (ztmin > xtmin) xtmin = ztmin;
-        if (ztmax < xtmax) xtmax = ztmax;
-        enter = (c1 & c2 & (xtmin < R.tmax) & (xtmax > tmin)) | ((meta.w & kNodeAlways) != 0);
-    }
-    // inner: descend to the near child, push the far one; leaf: stay on the node (leaf_step
-    // reads its primitive range); missed: pop, or done on an empty stack (sp is then dead).
-    // The far child is stored at level sp whatever the outcome (level sp is above the live
-    // stack unless it is pushed; the stack has depth + 1 levels), keeping the step branch-free.
-    const bool inner = enter && meta.y == 0;
-    const bool far_first = (R.neg >> meta.z) & 1u;
-    const uint32_t near_child = far_first ? meta.x : cur + 1;
-    const uint32_t far_child = far_first ? cur + 1 : meta.x;
-    st.put(static_cast<int>(sp), far_child);
-    R.cur = inner ? near_child : (enter ? cur : top);
-    R.sp = inner ? sp + 1 : (enter ? sp : sp - 1);
-    R.state = enter ? (meta.y ? kLeaf : kWalk) : (sp ? kWalk : kDone);
+    R.cur = cur;
+    R.sp = sp;
 }
 
 // the entered leaf's primitives in order (bvh.h:635-652), then "return" to the DFS.
@@ -446,6 +492,7 @@ __device__ __forceinline__ void leaf_step(const SceneView& S, Stack<SE>& st, con
                                           Trav& R, Counters& ctr) {
     const uint2 range = reinterpret_cast<const uint2*>(S.nodes + R.cur)[6];  // index, count
     const uint32_t end = range.x + range.y;
+    const double ia = recip_a(R.a);
     if (sphere_only) {
         DevSphere cur = S.spheres[range.x];
         for (uint32_t i = range.x; i < end; ++i) {
@@ -455,7 +502,7 @@ __device__ __forceinline__ void leaf_step(const SceneView& S, Stack<SE>& st, con
                 if (wave_leader()) ctr.it_leaf++;
             }
             double t;
-            if (hit_sphere(cur, o, d, R.a, tmin, R.tmax, t)) {
+            if (hit_sphere(cur, o, d, R.a, ia, tmin, R.tmax, t)) {
                 R.tmax = t;
                 R.ref = i;
                 R.found = true;
@@ -473,7 +520,7 @@ __device__ __forceinline__ void leaf_step(const SceneView& S, Stack<SE>& st, con
                 h = hit_quad(S.quads[ref & ~kRefQuad], o, d, tmin, R.tmax, t);
             } else {
                 if (COUNT) ctr.sphere_tests++;
-                h = hit_sphere(S.spheres[ref], o, d, R.a, tmin, R.tmax, t);
+                h = hit_sphere(S.spheres[ref], o, d, R.a, ia, tmin, R.tmax, t);
             }
             if (h) {
                 R.tmax = t;
@@ -623,13 +670,12 @@ __device__ __forceinline__ void stage_lds(unsigned char* dst, const void* src, u
 }
 
 // The render kernel. Thread -> (sample chunk, pixel); each wave starts on one 8x8 pixel tile.
-// Persistent per-lane state machine (WALK -> LEAF -> ... -> DONE -> shade -> WALK): every
-// iteration each walking lane visits one BVH node; lanes that entered a leaf park until at least
-// kLeafBatch of them hold one (or nobody walks), then test their leaves together; lanes whose ray
-// is finished park until kShadeBatch of them are finished (or nobody traverses), then shade
-// together, and a finished path starts the lane's next sample at once (path regeneration). So
-// the expensive leaf and shading code runs with many lanes active while the others keep
-// walking, and a wave is never held by its slowest ray or path.
+// Persistent per-lane state machine (WALK -> LEAF -> ... -> DONE -> shade -> WALK) in traversal
+// rounds: every walking lane walks the DFS to its next entered leaf (or the end of its
+// traversal), then the lanes holding a leaf test it together. Lanes whose ray is finished park
+// until kShadeBatch of them are finished (or nobody traverses), then shade together, and a
+// finished path starts the lane's next sample at once (path regeneration). So the shading code
+// runs with many lanes active, and a wave is never held by its slowest ray or path.
 // Samples are summed in sample order into partial[chunk][pixel].
 // LSCENE: nodes, primitive refs, spheres and parallelograms are staged in LDS first.
 #ifndef CRT_WAVES_PER_EU
@@ -638,14 +684,7 @@ __device__ __forceinline__ void stage_lds(unsigned char* dst, const void* src, u
 #ifndef CRT_SHADE_BATCH
 #define CRT_SHADE_BATCH 32
 #endif
-#ifndef CRT_LEAF_BATCH
-#define CRT_LEAF_BATCH 24
-#endif
-#ifndef CRT_SCHED
-#define CRT_SCHED 0  // 0: traversal rounds + batched shading; 1: node-level state machine
-#endif
 constexpr int kShadeBatch = CRT_SHADE_BATCH;
-[[maybe_unused]] constexpr int kLeafBatch = CRT_LEAF_BATCH;
 
 template <typename SE, bool GSTACK, bool LSCENE, bool COUNT>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRT_WAVES_PER_EU, 8))) void render_kernel(
@@ -698,15 +737,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRT_WAVE
     }
     unsigned long long cw = 0, cl = 0, cs = 0;
     while (true) {
-#if CRT_SCHED == 0
         // traversal rounds (walk to the next entered leaf, test it) until enough lanes hold a
         // finished ray, or none is traversing
         while (true) {
             if (COUNT) cw -= wall_clock64();
             if (!W.exact_slab && __ballot(R.state == kWalk && (R.neg & kZeroDir)) == 0) {
-                while (R.state == kWalk) walk_step<SE, COUNT, false>(S, st, P.o, C.t_min, R, ctr);
+                if (R.state == kWalk) walk<SE, COUNT, false>(S, st, P.o, C.t_min, R, ctr);
             } else {
-                while (R.state == kWalk) walk_step<SE, COUNT, true>(S, st, P.o, C.t_min, R, ctr);
+                if (R.state == kWalk) walk<SE, COUNT, true>(S, st, P.o, C.t_min, R, ctr);
             }
             if (COUNT) cw += wall_clock64();
             if (COUNT) cl -= wall_clock64();
@@ -719,25 +757,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRT_WAVE
         const uint64_t m_done = __ballot(R.state == kDone);
         if (m_done == 0) break;  // every lane idle: the chunk is finished
         {
-#else
-        // walk: one BVH node for every walking lane
-        if (COUNT) cw -= wall_clock64();
-        if (R.state == kWalk) walk_step<SE, COUNT, true>(S, st, P.o, C.t_min, R, ctr);
-        if (COUNT) cw += wall_clock64();
-        const uint64_t m_walk = __ballot(R.state == kWalk);
-        const uint64_t m_leaf = __ballot(R.state == kLeaf);
-        // leaf batch: once enough lanes hold an entered leaf, or nobody walks any more
-        if (m_leaf != 0 && (__popcll(m_leaf) >= kLeafBatch || m_walk == 0)) {
-            if (COUNT) cl -= wall_clock64();
-            if (R.state == kLeaf) leaf_step<SE, COUNT>(S, st, P.o, P.d, C.t_min, W.sphere_only != 0, R, ctr);
-            if (COUNT) cl += wall_clock64();
-        }
-        const uint64_t m_busy = __ballot(R.state == kWalk || R.state == kLeaf);
-        const uint64_t m_done = __ballot(R.state == kDone);
-        if (m_done == 0 && m_busy == 0) break;  // every lane idle: the chunk is finished
-        // shade batch: once enough rays are finished, or nobody traverses any more
-        if (m_done != 0 && (__popcll(m_done) >= kShadeBatch || m_busy == 0)) {
-#endif
             if (COUNT) cs -= wall_clock64();
             if (R.state == kDone) {
                 if (COUNT && wave_leader()) ctr.it_shade++;
@@ -1053,6 +1072,10 @@ static int launch_render(const crt_scene* s, int device, const crt_camera* cam, 
         count_stats->wave_iters_walk = h.it_walk;
         count_stats->wave_iters_leaf = h.it_leaf;
         count_stats->wave_iters_shade = h.it_shade;
+        if (std::getenv("CRT_DEBUG_COUNTERS"))
+            std::fprintf(stderr, "crt counters: rays %llu nodes %llu sphere_tests %llu quad_tests %llu it_walk %llu "
+                         "it_leaf %llu it_shade %llu\n", h.rays, h.nodes, h.sphere_tests, h.quad_tests, h.it_walk,
+                         h.it_leaf, h.it_shade);
     }
     return CRT_OK;
 }

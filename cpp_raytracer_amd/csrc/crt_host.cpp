@@ -358,6 +358,11 @@ static void stage(crt_scene* s) {
         for (int k = 0; k < 3; ++k)
             if (!(n.bounds[2 * k] <= n.bounds[2 * k + 1]) && !(n.flags & kNodeAlways)) s->exact_slab = true;
         std::memcpy(d.b, n.bounds, sizeof d.b);
+        if (n.flags & kNodeAlways)  // the render walk's min/max slab enters [-inf, inf] unconditionally
+            for (int k = 0; k < 3; ++k) {
+                d.b[2 * k] = -std::numeric_limits<double>::infinity();
+                d.b[2 * k + 1] = std::numeric_limits<double>::infinity();
+            }
         d.index = n.index;
         d.count = n.count;
         d.axis = n.axis;
