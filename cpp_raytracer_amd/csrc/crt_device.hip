@@ -206,9 +206,14 @@ __device__ __forceinline__ double div_a(double n, double a, double ia) {
 // spheres that cannot be accepted; only those are skipped, so the accepted roots are exactly the
 // reference's. NaN/inf anywhere makes the bound inconclusive and falls through to the exact test.
 // The sqrt and the two divisions by a are the correctly rounded ones (sqrt_from_rsq, div_a with
-// ia = recip_a(a)).
+// ia = recip_a(a)); lo / hi are lim_tmin / lim_tmax of the current t_min / t_max.
+// Coarse-reject limits of hit_sphere: t * a scaled outward by 2^-30 (tmin side: inward).
+__device__ __forceinline__ double lim_tmax(double tmax, double a) { return tmax * a * (1 + 0x1p-30); }
+__device__ __forceinline__ double lim_tmin(double tmin, double a) { return tmin * a * (1 - 0x1p-30); }
+
 __device__ __forceinline__ bool hit_sphere(const DevSphere& sp, const double o[3], const double d[3],
-                                           double a, double ia, double tmin, double tmax, double& t) {
+                                           double a, double ia, double tmin, double tmax, double lo,
+                                           double hi, double& t) {
     double ocx = o[0] - sp.c[0], ocy = o[1] - sp.c[1], ocz = o[2] - sp.c[2];
     double b = d[0] * ocx + d[1] * ocy + d[2] * ocz;
     double c = (ocx * ocx + ocy * ocy + ocz * ocz) - sp.r * sp.r;
@@ -218,8 +223,8 @@ __device__ __forceinline__ bool hit_sphere(const DevSphere& sp, const double o[3
     {
         const double sqa = disc * rs;                              // ~sqrt(disc)
         const double m = (fabs(b) + sqa) * 0x1p-12;                // covers every rounding error
-        const bool beyond = (-b - sqa) - m > tmax * a * (1 + 0x1p-30);   // r1 > tmax, so r2 too
-        const bool before = (-b + sqa) + m < tmin * a * (1 - 0x1p-30);   // r2 < tmin, so r1 too
+        const bool beyond = (-b - sqa) - m > hi;   // r1 > tmax, so r2 too  (hi = lim_tmax)
+        const bool before = (-b + sqa) + m < lo;   // r2 < tmin, so r1 too  (lo = lim_tmin)
         if (beyond || before) return false;
     }
     double sq = sqrt_from_rsq(disc, rs);
@@ -313,7 +318,8 @@ __device__ __forceinline__ bool trace(const SceneView& S, Stack<SE>& st, const d
     const double inv[3] = {1 / d[0], 1 / d[1], 1 / d[2]};
     const uint32_t neg = (d[0] < 0 ? 1u : 0u) | (d[1] < 0 ? 2u : 0u) | (d[2] < 0 ? 4u : 0u);
     const double a = d[0] * d[0] + d[1] * d[1] + d[2] * d[2];  // dot(ray.dir, ray.dir)
-    const double ia = recip_a(a);
+    const double ia = recip_a(a), lo = lim_tmin(tmin, a);
+    double hi = lim_tmax(tmax, a);
     bool found = false;
     int sp = 0;
     uint32_t cur = 0;
@@ -354,10 +360,11 @@ __device__ __forceinline__ bool trace(const SceneView& S, Stack<SE>& st, const d
                 h = hit_quad(S.quads[ref & ~kRefQuad], o, d, tmin, tmax, t);
             } else {
                 if (COUNT) ctr.sphere_tests++;
-                h = hit_sphere(S.spheres[ref], o, d, a, ia, tmin, tmax, t);
+                h = hit_sphere(S.spheres[ref], o, d, a, ia, tmin, tmax, lo, hi, t);
             }
             if (h) {
                 tmax = t;
+                hi = lim_tmax(t, a);
                 hit_ref = ref;
                 found = true;
             }
@@ -492,18 +499,22 @@ __device__ __forceinline__ void leaf_step(const SceneView& S, Stack<SE>& st, con
                                           Trav& R, Counters& ctr) {
     const uint2 range = reinterpret_cast<const uint2*>(S.nodes + R.cur)[6];  // index, count
     const uint32_t end = range.x + range.y;
-    const double ia = recip_a(R.a);
+    const double ia = recip_a(R.a), lo = lim_tmin(tmin, R.a);
+    double hi = lim_tmax(R.tmax, R.a);
     if (sphere_only) {
         DevSphere cur = S.spheres[range.x];
         for (uint32_t i = range.x; i < end; ++i) {
-            const DevSphere nxt = S.spheres[i + 1 < end ? i + 1 : i];
+            // one past the leaf's last sphere is still inside the scene copy (sphere_mat follows
+            // the spheres in HBM, the parallelogram / stack regions in LDS); it is never tested
+            const DevSphere nxt = S.spheres[i + 1];
             if (COUNT) {
                 ctr.sphere_tests++;
                 if (wave_leader()) ctr.it_leaf++;
             }
             double t;
-            if (hit_sphere(cur, o, d, R.a, ia, tmin, R.tmax, t)) {
+            if (hit_sphere(cur, o, d, R.a, ia, tmin, R.tmax, lo, hi, t)) {
                 R.tmax = t;
+                hi = lim_tmax(t, R.a);
                 R.ref = i;
                 R.found = true;
             }
@@ -520,10 +531,11 @@ __device__ __forceinline__ void leaf_step(const SceneView& S, Stack<SE>& st, con
                 h = hit_quad(S.quads[ref & ~kRefQuad], o, d, tmin, R.tmax, t);
             } else {
                 if (COUNT) ctr.sphere_tests++;
-                h = hit_sphere(S.spheres[ref], o, d, R.a, ia, tmin, R.tmax, t);
+                h = hit_sphere(S.spheres[ref], o, d, R.a, ia, tmin, R.tmax, lo, hi, t);
             }
             if (h) {
                 R.tmax = t;
+                hi = lim_tmax(t, R.a);
                 R.ref = ref;
                 R.found = true;
             }
