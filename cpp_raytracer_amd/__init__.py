@@ -23,7 +23,7 @@ from ._capi import (CRT_BOX, CRT_DIELECTRIC, CRT_DIFFUSE_LIGHT, CRT_LAMBERTIAN, 
 
 __all__ = [
     "SceneData", "GpuScene", "CameraSettings", "Camera", "Tiling", "RenderStats", "CrtError",
-    "resolve_camera", "sample_seed", "rand_double", "device_count", "lib",
+    "resolve_camera", "sample_seed", "rand_double", "device_count", "lib", "ppm_values", "write_ppm",
     "CRT_LAMBERTIAN", "CRT_METAL", "CRT_DIELECTRIC", "CRT_DIFFUSE_LIGHT",
     "CRT_SPHERE", "CRT_PARALLELOGRAM", "CRT_BOX",
 ]
@@ -47,6 +47,22 @@ def device_count() -> int:
     n = C.c_int(0)
     rc = lib().crt_device_count(C.byref(n))
     return n.value if rc == 0 else 0
+
+
+def ppm_values(device: int, frame_ptr: int, height: int, width: int, stream: int = 0) -> np.ndarray:
+    """Image::send_as_ppm's integers (h, w, 3 int32) for a device frame of h*w RGB f64 pixels
+    (crt_ppm_values: computed on the GPU)."""
+    out = np.zeros((height, width, 3), np.int32)
+    check(lib().crt_ppm_values(device, C.c_void_p(frame_ptr), height * width, out.ctypes.data,
+                               C.c_void_p(stream)), "crt_ppm_values")
+    return out
+
+
+def write_ppm(path, values: np.ndarray) -> None:
+    """Writes (h, w, 3) integers as Image::send_as_ppm does (crt_ppm_write)."""
+    v = np.ascontiguousarray(values, np.int32)
+    h, w, _ = v.shape
+    check(lib().crt_ppm_write(str(path).encode(), w, h, v.ctypes.data), "crt_ppm_write")
 
 
 def _settings_bytes(cs: CameraSettings) -> bytes:

@@ -119,6 +119,8 @@ EXPORTS = {
     "crt_render": (C.c_int, [C.c_void_p, P(Camera), C.c_int, C.c_void_p, P(RenderStats)]),
     "crt_closest_hits": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t, C.c_double, C.c_double,
                                    C.c_void_p]),
+    "crt_ppm_values": (C.c_int, [C.c_int, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p]),
+    "crt_ppm_write": (C.c_int, [C.c_char_p, C.c_uint32, C.c_uint32, C.c_void_p]),
 }
 
 

@@ -839,6 +839,42 @@ __global__ __launch_bounds__(256) void resolve_kernel(const double* __restrict__
     out[pix * 3 + 2] = b * inv_spp;
 }
 
+// Image::send_as_ppm's integers (image.h:38-56; RGB::as_string rgb.h:99-115 with its defaults):
+// Reinhard by luminance (rgb.h:27-29), gamma 2, static_cast<int>(255.999999 * .). The reference
+// takes std::pow(x, 1/2) (rgb.h:10-13), a libm pow within ~1 ulp of the correctly rounded sqrt
+// used here; where the truncated integer could differ for any value within 2 ulps of sqrt(x)
+// (or v is NaN / out of int range), the kernel writes kPpmRedo and the host recomputes that
+// pixel with std::pow (device_ppm_values), so every integer is the reference's.
+constexpr double kPpmScale = 255 + 0.999999;
+constexpr int32_t kPpmRedo = INT32_MIN + 1;
+
+__global__ __launch_bounds__(256) void ppm_kernel(const double* __restrict__ rgb, uint64_t n,
+                                                  int32_t* __restrict__ out) {
+    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * 256 + threadIdx.x;
+    if (i >= n) return;
+    const double c[3] = {rgb[3 * i], rgb[3 * i + 1], rgb[3 * i + 2]};
+    const double L = 0.2126 * c[0] + 0.7152 * c[1] + 0.0722 * c[2];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const double x = c[k] / (1 + L);
+        const double s = sqrt(x);
+        const double v = kPpmScale * s;
+        int32_t q;
+        if (!(v >= 0 && v < 2147483648.0)) {
+            q = kPpmRedo;
+        } else if (s < 0x1p-1000) {
+            q = 0;  // pow(x, 0.5) is below 2^-999 too
+        } else {
+            const uint64_t bits = static_cast<uint64_t>(__double_as_longlong(s));
+            const double lo = __longlong_as_double(static_cast<long long>(bits - 2));
+            const double hi = __longlong_as_double(static_cast<long long>(bits + 2));
+            q = static_cast<int32_t>(kPpmScale * lo) == static_cast<int32_t>(kPpmScale * hi)
+                    ? static_cast<int32_t>(v) : kPpmRedo;
+        }
+        out[3 * i + k] = q;
+    }
+}
+
 // Closest-hit queries (BVH::hit_by for an arbitrary ray batch).
 __global__ __launch_bounds__(kBlock) void hits_kernel(SceneView S, const double* __restrict__ rays,
                                                       uint32_t n, double t_min, double t_max,
@@ -1209,6 +1245,40 @@ int device_closest_hits(crt_scene* s, int device, const double* rays, size_t n, 
     (void)hipFree(d_stack);
     if (le != hipSuccess) return fail(CRT_E_HIP, std::string("hits_kernel launch: ") + hipGetErrorString(le));
     if (se != hipSuccess) return fail(CRT_E_HIP, std::string("hits_kernel: ") + hipGetErrorString(se));
+    return CRT_OK;
+}
+
+int device_ppm_values(int device, const double* d_rgb, size_t n, int32_t* h_values, void* stream) {
+    int rc = check_device(device);
+    if (rc) return rc;
+    if (n == 0) return CRT_OK;
+    if (n > (1ull << 40)) return fail(CRT_E_INVALID, "crt_ppm_values: frame too large");
+    DeviceGuard g(device);
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    int32_t* d_out = nullptr;
+    HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&d_out), n * 3 * sizeof(int32_t), st));
+    hipLaunchKernelGGL(dev::ppm_kernel, dim3(static_cast<uint32_t>((n + 255) / 256)), dim3(256), 0, st,
+                       d_rgb, static_cast<uint64_t>(n), d_out);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipMemcpyAsync(h_values, d_out, n * 3 * sizeof(int32_t), hipMemcpyDeviceToHost, st);
+    (void)hipFreeAsync(d_out, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) return fail(CRT_E_HIP, std::string("ppm_kernel: ") + hipGetErrorString(e));
+    // pixels the kernel could not settle: recompute on the host with std::pow
+    std::vector<size_t> redo;
+    for (size_t p = 0; p < n; ++p)
+        if (h_values[3 * p] == dev::kPpmRedo || h_values[3 * p + 1] == dev::kPpmRedo ||
+            h_values[3 * p + 2] == dev::kPpmRedo)
+            redo.push_back(p);
+    if (redo.empty()) return CRT_OK;
+    std::vector<double> px(redo.size() > 4096 ? n * 3 : 3);
+    if (redo.size() > 4096) HIP_TRY(hipMemcpy(px.data(), d_rgb, n * 3 * sizeof(double), hipMemcpyDeviceToHost));
+    for (size_t p : redo) {
+        const double* src = px.data();
+        if (redo.size() > 4096) src += 3 * p;
+        else HIP_TRY(hipMemcpy(px.data(), d_rgb + 3 * p, 3 * sizeof(double), hipMemcpyDeviceToHost));
+        ppm_pixel_host(src, h_values + 3 * p);
+    }
     return CRT_OK;
 }
 

@@ -7,6 +7,8 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdint>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <limits>
@@ -346,6 +348,20 @@ static int build_bvh(crt_scene* s, const crt_bvh_params& prm) {
     s->build_ms =
         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return CRT_OK;
+}
+
+// RGB::as_string (rgb.h:99-115) with its defaults as the x86-64 reference build computes it:
+// std::pow(x, 1 / gamma) with gamma = 2 taken at run time (a libm pow, as in the reference),
+// static_cast<int> as cvttsd2si (NaN / out of range -> INT_MIN).
+static volatile double g_ppm_gamma = 2;
+
+void ppm_pixel_host(const double rgb[3], int32_t out[3]) {
+    const double gamma = g_ppm_gamma, scale = 255 + 0.999999;
+    const double L = 0.2126 * rgb[0] + 0.7152 * rgb[1] + 0.0722 * rgb[2];
+    for (int k = 0; k < 3; ++k) {
+        const double v = scale * std::pow(rgb[k] / (1 + L), 1 / gamma);
+        out[k] = (v > -2147483649.0 && v < 2147483648.0) ? static_cast<int32_t>(v) : INT32_MIN;
+    }
 }
 
 // device-layout staging arrays
@@ -993,6 +1009,35 @@ int crt_render(crt_scene* s, const crt_camera* cam, int num_devices, double* h_r
     clear_error();
     if (!s || !cam || !h_rgb) return fail(CRT_E_INVALID, "crt_render: null argument");
     return render_multi(s, cam, num_devices, h_rgb, stats);
+}
+
+int crt_ppm_values(int device, const double* d_rgb, size_t n, int32_t* h_values, void* stream) {
+    clear_error();
+    if (n && (!d_rgb || !h_values)) return fail(CRT_E_INVALID, "crt_ppm_values: null argument");
+    return device_ppm_values(device, d_rgb, n, h_values, stream);
+}
+
+int crt_ppm_write(const char* path, uint32_t w, uint32_t h, const int32_t* values) {
+    clear_error();
+    if (!path || (static_cast<uint64_t>(w) * h && !values)) return fail(CRT_E_INVALID, "crt_ppm_write: null argument");
+    std::FILE* f = std::fopen(path, "wb");
+    if (!f) return fail(CRT_E_INVALID, std::string("crt_ppm_write: could not open the file \"") + path + "\"");
+    std::string buf = "P3\n" + std::to_string(w) + " " + std::to_string(h) + "\n255\n";
+    const uint64_t n = static_cast<uint64_t>(w) * h;
+    bool ok = true;
+    for (uint64_t p = 0; p < n && ok; ++p) {
+        for (int k = 0; k < 3; ++k) {
+            buf += std::to_string(values[3 * p + k]);
+            buf += k < 2 ? ' ' : '\n';
+        }
+        if (buf.size() > (1u << 20)) {
+            ok = std::fwrite(buf.data(), 1, buf.size(), f) == buf.size();
+            buf.clear();
+        }
+    }
+    if (ok && !buf.empty()) ok = std::fwrite(buf.data(), 1, buf.size(), f) == buf.size();
+    ok = (std::fclose(f) == 0) && ok;
+    return ok ? CRT_OK : fail(CRT_E_INVALID, std::string("crt_ppm_write: write failed: ") + path);
 }
 
 int crt_closest_hits(crt_scene* s, int device, const double* rays, size_t n, double t_min,

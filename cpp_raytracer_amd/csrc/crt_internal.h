@@ -115,6 +115,9 @@ int device_render(const crt_scene* s, int device, const crt_camera* cam, const c
 int device_closest_hits(crt_scene* s, int device, const double* rays, size_t n, double t_min,
                         double t_max, crt_hit* out);
 int device_count(int* n);
+int device_ppm_values(int device, const double* d_rgb, size_t n, int32_t* h_values, void* stream);
+// host: RGB::as_string's three integers for one pixel (std::pow, x86 int conversion)
+void ppm_pixel_host(const double rgb[3], int32_t out[3]);
 int render_multi(crt_scene* s, const crt_camera* cam, int num_devices, double* h_rgb,
                  crt_render_stats* stats);
 }  // namespace crt

@@ -226,6 +226,17 @@ int crt_render(crt_scene* scene, const crt_camera* cam, int num_devices, double*
 int crt_closest_hits(crt_scene* scene, int device, const double* rays, size_t n,
                      double t_min, double t_max, crt_hit* out);
 
+/* The integers Image::send_as_ppm prints (image.h:38-56; RGB::as_string rgb.h:99-115 with its
+ * defaults: Reinhard tone map by luminance, gamma 2, static_cast<int>(255.999999 * v)) for the
+ * n-pixel frame d_rgb (device memory on `device`, row-major RGB f64, e.g. crt_render_async's
+ * output), computed on the GPU; h_values (host, 3n int32) receives them, identical to the
+ * x86-64 reference build's (NaN / out of range -> INT_MIN). Synchronous on `stream`. */
+int crt_ppm_values(int device, const double* d_rgb, size_t n, int32_t* h_values, void* stream);
+
+/* Writes w x h pixel values (3 per pixel) as Image::send_as_ppm does: "P3\nw h\n255\n", then
+ * one "r g b\n" line per pixel, rows top to bottom. */
+int crt_ppm_write(const char* path, uint32_t w, uint32_t h, const int32_t* values);
+
 #ifdef __cplusplus
 }
 #endif

@@ -665,3 +665,24 @@ int oracle_hits(const crt_material* mats, size_t nm, const crt_object* objs, siz
     world_free(&w);
     return 0;
 }
+
+/* ---- Image::send_as_ppm values (image.h:38-56, rgb.h:10-13, 27-29, 99-115) ------------- */
+static volatile double g_gamma = 2; /* runtime exponent: keeps pow(x, 1/gamma) a libm pow call */
+
+static int32_t to_int_x86(double v) { /* static_cast<int> as cvttsd2si */
+    if (!(v > -2147483649.0 && v < 2147483648.0)) return INT32_MIN;
+    return (int32_t)v;
+}
+
+void oracle_ppm_values(const double* rgb, size_t n, int32_t* out) {
+    const double gamma = g_gamma, scale = 255 + 0.999999;
+    for (size_t i = 0; i < n; ++i) {
+        const double r = rgb[3 * i], g = rgb[3 * i + 1], b = rgb[3 * i + 2];
+        const double L = 0.2126 * r + 0.7152 * g + 0.0722 * b;
+        double c[3] = {r, g, b};
+        for (int k = 0; k < 3; ++k) {
+            c[k] /= 1 + L;
+            out[3 * i + k] = to_int_x86(scale * pow(c[k], 1 / gamma));
+        }
+    }
+}

@@ -48,6 +48,12 @@ int oracle_hits(const crt_material* mats, size_t nm, const crt_object* objs, siz
 
 uint32_t oracle_sample_seed(uint32_t base, uint32_t pixel, uint32_t sample);
 
+/* The integers Image::send_as_ppm prints (image.h:38-56) for n RGB pixels: RGB::as_string
+ * (rgb.h:99-115) with its defaults — Reinhard by luminance (rgb.h:27-29), gamma 2 via
+ * std::pow(x, 1/2) (rgb.h:10-13), static_cast<int>(255.999999 * .) — as the x86-64 g++ build
+ * computes them (cvttsd2si: NaN / out of range -> INT_MIN). out: 3n values. */
+void oracle_ppm_values(const double* rgb, size_t n, int32_t* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -31,6 +31,7 @@ def lib():
         _lib.oracle_camera.argtypes = [vp, vp]
         _lib.oracle_sample_seed.argtypes = [u32, u32, u32]
         _lib.oracle_sample_seed.restype = u32
+        _lib.oracle_ppm_values.argtypes = [vp, sz, vp]
     return _lib
 
 
@@ -84,6 +85,14 @@ def hits(scene, rays, t_min=1e-5, t_max=float("inf")):
     out = np.zeros(len(rays), HIT_DTYPE)
     lib().oracle_hits(m.ctypes.data, len(m), o.ctypes.data, len(o), rays.ctypes.data, len(rays), t_min, t_max,
                       out.ctypes.data)
+    return out
+
+
+def ppm_values(frame):
+    """Image::send_as_ppm's integers for an (..., 3) f64 frame (same leading shape, int32)."""
+    f = np.ascontiguousarray(frame, np.float64)
+    out = np.zeros(f.shape, np.int32)
+    lib().oracle_ppm_values(f.ctypes.data, f.size // 3, out.ctypes.data)
     return out
 
 

@@ -13,6 +13,8 @@
  *   hits    <scene> <rays> <out>         BVH::hit_by closest hits          (bvh.h:585-715)
  *   time    <scene> <threads> [rows]     unmodified Camera::render timing  (CPU baseline)
  *   refsum  <scene> <seed>               1-thread unmodified render checksum (shim check)
+ *   ppm     <frame.f64> <h> <w> <out.ppm>  Image::send_as_ppm of a raw row-major f64 RGB frame
+ *                                        (image.h:38-56, RGB::as_string rgb.h:99-115)
  *
  * The reference's Camera keeps init/random_ray_through_pixel/ray_color private (implicit
  * `class` access); the driver reaches them by including every standard header first and then
@@ -201,6 +203,25 @@ int main(int argc, char** argv) {
     // the reference prints progress bars and BVH stats on stdout; keep our own output on fd 3
     // by writing results to files, and send the reference's chatter to stderr.
     std::cout.rdbuf(std::cerr.rdbuf());
+    if (mode == "ppm") {
+        if (argc < 6) return 2;
+        std::vector<char> raw;
+        {
+            std::ifstream g(argv[2], std::ios::binary);
+            raw.assign(std::istreambuf_iterator<char>(g), {});
+        }
+        size_t h = std::strtoul(argv[3], nullptr, 10), w = std::strtoul(argv[4], nullptr, 10);
+        if (raw.size() != h * w * 3 * sizeof(double)) { std::fprintf(stderr, "ppm: size mismatch\n"); return 2; }
+        const double* f = reinterpret_cast<const double*>(raw.data());
+        std::vector<std::vector<RGB>> px(h, std::vector<RGB>(w, RGB::zero()));
+        for (size_t r = 0; r < h; ++r)
+            for (size_t c = 0; c < w; ++c) {
+                const double* q = f + (r * w + c) * 3;
+                px[r][c] = RGB::from_mag(q[0], q[1], q[2]);
+            }
+        Image(px).send_as_ppm(argv[5]);
+        return 0;
+    }
     Loaded L = load(argv[2]);
     if (mode == "camera") {
         Camera cam = make_camera(L.cs);

@@ -75,6 +75,47 @@ def scene_digest(d: crt.SceneData) -> str:
     return hashlib.sha256(d.materials.tobytes() + d.objects.tobytes()).hexdigest()
 
 
+def ppm_edge_frame() -> np.ndarray:
+    """64x64 frame for the PPM-value goldens: ordinary colours, NaN / inf / -0 / denormals /
+    huge values, and pixels whose gamma-encoded value lands within a few ulps of an integer
+    after scaling (where sqrt and pow(x, 0.5) could truncate differently)."""
+    rng = np.random.default_rng(99)
+    f = rng.uniform(0, 3, (64, 64, 3))
+    flat = f.reshape(-1, 3)
+    specials = [np.nan, np.inf, -np.inf, -0.0, 0.0, 5e-324, 1e-310, 1e300, -1.0, 1e-8]
+    for i, v in enumerate(specials):
+        flat[i] = [v, 0.5, 0.25]
+        flat[len(specials) + i] = [0.5, v, v]
+    scale = 255 + 0.999999
+    k0 = 2 * len(specials)
+    for j, k in enumerate(range(0, 700)):
+        x2 = (k / scale) ** 2                      # r / (1 + L) with g = b = 0
+        r = x2 / (1 - 0.2126 * x2) if x2 < 1 / 0.2126 else 1e9
+        r = np.nextafter(r, np.inf) if j % 3 == 1 else (np.nextafter(r, -np.inf) if j % 3 == 2 else r)
+        flat[k0 + j] = [r, 0.0, 0.0]
+    return f
+
+
+def gen_ppm(tmp: Path) -> None:
+    """Image::send_as_ppm integers (oracle/_ref ppm mode) for the config-1 golden render and the
+    edge frame."""
+    cases = {"config1": np.load(GOLD / "render_config1.npz")["rgb"], "edges": ppm_edge_frame()}
+    out = {}
+    for name, frame in cases.items():
+        h, w, _ = frame.shape
+        src, dst = tmp / f"{name}.f64", tmp / f"{name}.ppm"
+        src.write_bytes(np.ascontiguousarray(frame, "<f8").tobytes())
+        run("ppm", src, h, w, dst)
+        text = dst.read_text().split("\n")
+        assert text[0] == "P3" and text[1] == f"{w} {h}" and text[2] == "255"
+        vals = np.array([list(map(int, ln.split())) for ln in text[3:3 + h * w]], np.int64)
+        out[f"{name}_values"] = vals.reshape(h, w, 3).astype(np.int32)
+        if name == "edges":
+            out["edges_frame"] = frame
+        out[f"{name}_sha256"] = np.frombuffer(hashlib.sha256(dst.read_bytes()).digest(), np.uint8)
+    np.savez_compressed(GOLD / "ppm_cases.npz", **out)
+
+
 def main() -> None:
     subprocess.run(["make", "-C", str(ROOT / "oracle"), "ref"], check=True)
     meta = {"generator": "tests/golden/gen_golden.py", "reference": "DeltaPavonis/cpp_raytracer (oracle/_ref)",
@@ -134,9 +175,15 @@ def main() -> None:
             out = tmp / "h.npy"
             run("hits", p, rays_path, out)
             np.savez_compressed(GOLD / f"hits_{name}.npz", rays=rays, hits=np.load(out))
+        gen_ppm(tmp)
     (GOLD / "golden.json").write_text(json.dumps(meta, indent=1, sort_keys=True))
     print("golden fixtures written to", GOLD)
 
 
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["ppm"]:  # only the PPM-value fixtures
+        subprocess.run(["make", "-C", str(ROOT / "oracle"), "ref"], check=True)
+        with tempfile.TemporaryDirectory() as td:
+            gen_ppm(Path(td))
+    else:
+        main()
