@@ -143,15 +143,17 @@ def camera_with(settings: CameraSettings, **kw) -> CameraSettings:
 
 
 class GpuScene:
-    """A flattened scene + reference-order BVH (host) with per-device HBM copies."""
+    """A flattened scene + reference-order BVH with per-device HBM copies. The BVH is built on
+    the host, or on GPU `build_device` (the same tree, crt_bvh_params.build_device)."""
 
     def __init__(self, data: SceneData, num_buckets: int = 32, max_prims_in_node: int = 12,
-                 linear: bool = False):
+                 linear: bool = False, build_device: Optional[int] = None):
         self.data = data
         self._h = C.c_void_p()
         mats = np.ascontiguousarray(data.materials, dtype=MATERIAL_DTYPE)
         objs = np.ascontiguousarray(data.objects, dtype=OBJECT_DTYPE)
-        prm = BVHParams(num_buckets, max_prims_in_node, int(linear), 0)
+        prm = BVHParams(num_buckets, max_prims_in_node, int(linear),
+                        0 if build_device is None else build_device + 1)
         check(lib().crt_scene_create(mats.ctypes.data, len(mats), objs.ctypes.data, len(objs),
                                      C.byref(prm), C.byref(self._h)), "crt_scene_create")
 

@@ -31,7 +31,7 @@ class Object(C.Structure):
 
 class BVHParams(C.Structure):
     _fields_ = [("num_buckets", C.c_uint32), ("max_prims_in_node", C.c_uint32),
-                ("linear", C.c_uint32), ("reserved", C.c_uint32)]
+                ("linear", C.c_uint32), ("build_device", C.c_uint32)]
 
 
 class CameraSettings(C.Structure):

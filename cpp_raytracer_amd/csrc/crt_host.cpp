@@ -18,6 +18,7 @@
 #include <optional>
 #include <random>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "crt_internal.h"
@@ -55,12 +56,46 @@ static inline V3 unit(V3 a) { return divv(a, mag(a)); }                         
 static inline V3 v3(const double* p) { return {p[0], p[1], p[2]}; }
 static inline void put(double* p, V3 a) { p[0] = a.x; p[1] = a.y; p[2] = a.z; }
 
+// std::fmin / std::fmax as the reference's g++ build evaluates them: calls into glibc, whose
+// x86-64 versions return the SECOND operand on a tie (so fmin(+0, -0) = -0) and the other operand
+// when one is NaN. clang inlines them with the operands commuted, which differs on signed zeros,
+// so the host code spells the glibc semantics out.
+static inline double gfmin(double x, double y) {
+    if (std::isnan(x)) return y;
+    if (std::isnan(y)) return x;
+    return x < y ? x : y;
+}
+static inline double gfmax(double x, double y) {
+    if (std::isnan(x)) return y;
+    if (std::isnan(y)) return x;
+    return x > y ? x : y;
+}
+
+// f(begin, end) over [0, n) in contiguous chunks on up to 16 threads (scene preparation of
+// multi-million-primitive scenes; every element is written by exactly one thread).
+template <typename F>
+static void parallel_for(size_t n, size_t min_chunk, F&& f) {
+    const size_t hw = std::max(1u, std::thread::hardware_concurrency());
+    const size_t nt = std::min<size_t>(std::min<size_t>(hw, 16), (n + min_chunk - 1) / min_chunk);
+    if (nt <= 1) {
+        f(size_t(0), n);
+        return;
+    }
+    const size_t per = (n + nt - 1) / nt;
+    std::vector<std::thread> th;
+    for (size_t t = 0; t < nt; ++t) {
+        const size_t a = t * per, b = std::min(n, a + per);
+        if (a < b) th.emplace_back([&f, a, b] { f(a, b); });
+    }
+    for (auto& x : th) x.join();
+}
+
 // ---- intervals / AABB (math/interval.h, acceleration/aabb.h) --------------------------------
 struct Iv {
     double min, max;
     double size() const { return max - min; }
-    void merge(const Iv& o) { min = std::fmin(min, o.min); max = std::fmax(max, o.max); }
-    void merge(double d) { min = std::fmin(min, d); max = std::fmax(max, d); }
+    void merge(const Iv& o) { min = gfmin(min, o.min); max = gfmax(max, o.max); }   // interval.h:45-54
+    void merge(double d) { min = gfmin(min, d); max = gfmax(max, d); }
     double mid() const { return std::midpoint(min, max); }                         // interval.h:31
 };
 constexpr double kInf = std::numeric_limits<double>::infinity();
@@ -131,49 +166,56 @@ static Prim make_quad(V3 v, V3 s1, V3 s2, uint32_t mat) {
     return p;
 }
 
+static void emit_object(const crt_object& o, Prim* out) {
+    switch (o.kind) {
+        case CRT_SPHERE:
+            out[0] = make_sphere(v3(o.v), o.v[3], o.material);
+            break;
+        case CRT_PARALLELOGRAM:
+            out[0] = make_quad(v3(o.v), v3(o.v + 3), v3(o.v + 6), o.material);
+            break;
+        default: {  // CRT_BOX, box.h:53-84: min/max corners, three sides, six faces in this order
+            double a0[3], a1[3];
+            for (int k = 0; k < 3; ++k) {
+                a0[k] = gfmin(o.v[k], o.v[3 + k]);   // box.h:64-65
+                a1[k] = gfmax(o.v[k], o.v[3 + k]);
+            }
+            const V3 mn = v3(a0), mx = v3(a1);
+            const V3 sx{mx.x - mn.x, 0, 0}, sy{0, mx.y - mn.y, 0}, sz{0, 0, mx.z - mn.z};
+            out[0] = make_quad(mn, sx, sy, o.material);
+            out[1] = make_quad(mn, sx, sz, o.material);
+            out[2] = make_quad(mn, sy, sz, o.material);
+            out[3] = make_quad(mx, neg(sx), neg(sy), o.material);
+            out[4] = make_quad(mx, neg(sx), neg(sz), o.material);
+            out[5] = make_quad(mx, neg(sy), neg(sz), o.material);
+            break;
+        }
+    }
+}
+
 static int flatten(crt_scene* s) {
-    s->prims.clear();
-    for (size_t i = 0; i < s->objects.size(); ++i) {
+    // validate in object order (first error wins), then emit in parallel at prefix offsets
+    const size_t no = s->objects.size();
+    std::vector<size_t> off(no + 1, 0);
+    for (size_t i = 0; i < no; ++i) {
         const crt_object& o = s->objects[i];
         if (o.material >= s->materials.size())
             return fail(CRT_E_INVALID, "object " + std::to_string(i) + " references material " +
                                            std::to_string(o.material) + " out of range");
-        switch (o.kind) {
-            case CRT_SPHERE:
-                s->prims.push_back(make_sphere(v3(o.v), o.v[3], o.material));
-                break;
-            case CRT_PARALLELOGRAM:
-                s->prims.push_back(make_quad(v3(o.v), v3(o.v + 3), v3(o.v + 6), o.material));
-                break;
-            case CRT_BOX: {
-                // box.h:53-84: min/max corners, three sides, six faces in this order
-                V3 mn, mx;
-                double a0[3], a1[3];
-                for (int k = 0; k < 3; ++k) {
-                    a0[k] = std::fmin(o.v[k], o.v[3 + k]);
-                    a1[k] = std::fmax(o.v[k], o.v[3 + k]);
-                }
-                mn = v3(a0);
-                mx = v3(a1);
-                V3 sx{mx.x - mn.x, 0, 0}, sy{0, mx.y - mn.y, 0}, sz{0, 0, mx.z - mn.z};
-                s->prims.push_back(make_quad(mn, sx, sy, o.material));
-                s->prims.push_back(make_quad(mn, sx, sz, o.material));
-                s->prims.push_back(make_quad(mn, sy, sz, o.material));
-                s->prims.push_back(make_quad(mx, neg(sx), neg(sy), o.material));
-                s->prims.push_back(make_quad(mx, neg(sx), neg(sz), o.material));
-                s->prims.push_back(make_quad(mx, neg(sy), neg(sz), o.material));
-                break;
-            }
-            default:
-                return fail(CRT_E_INVALID, "object " + std::to_string(i) + " has unknown kind " +
-                                               std::to_string(o.kind));
-        }
+        if (o.kind != CRT_SPHERE && o.kind != CRT_PARALLELOGRAM && o.kind != CRT_BOX)
+            return fail(CRT_E_INVALID, "object " + std::to_string(i) + " has unknown kind " +
+                                           std::to_string(o.kind));
+        off[i + 1] = off[i] + (o.kind == CRT_BOX ? 6 : 1);
     }
     for (size_t i = 0; i < s->materials.size(); ++i) {
         uint32_t k = s->materials[i].kind;
         if (k < CRT_LAMBERTIAN || k > CRT_DIFFUSE_LIGHT)
             return fail(CRT_E_INVALID, "material " + std::to_string(i) + " has unknown kind");
     }
+    s->prims.resize(off[no]);
+    parallel_for(no, 4096, [&](size_t a, size_t b) {
+        for (size_t i = a; i < b; ++i) emit_object(s->objects[i], s->prims.data() + off[i]);
+    });
     return CRT_OK;
 }
 
@@ -312,6 +354,15 @@ void flatten_tree(const TreeNode* t, std::vector<crt_bvh_node>& out, size_t& nex
 }
 }  // namespace
 
+// The GPU build reproduces the host fold only for NaN-free boxes (with a NaN, fmin/fmax pick by
+// operand order in ways the order-preserving keys do not model); those scenes build on the host.
+static bool gpu_buildable(const std::vector<Prim>& prims) {
+    for (const Prim& p : prims)
+        for (double v : p.box)
+            if (std::isnan(v)) return false;
+    return true;
+}
+
 static int build_bvh(crt_scene* s, const crt_bvh_params& prm) {
     auto t0 = std::chrono::steady_clock::now();
     const size_t n = s->prims.size();
@@ -337,6 +388,21 @@ static int build_bvh(crt_scene* s, const crt_bvh_params& prm) {
         s->nodes.push_back(e);
         s->depth = 1;
         s->max_leaf = static_cast<uint32_t>(n);
+    } else if (prm.build_device != 0 && gpu_buildable(s->prims)) {
+        // the same tree built on a GPU (crt_bvh_gpu.hip); boxes and centroids as Builder's
+        std::vector<double> bx(n * 6), cc(n * 3);
+        parallel_for(n, 8192, [&](size_t a, size_t b) {
+            for (size_t i = a; i < b; ++i) {
+                std::memcpy(&bx[6 * i], s->prims[i].box, 6 * sizeof(double));
+                const V3 c = box_of(s->prims[i].box).centroid();
+                cc[3 * i] = c.x;
+                cc[3 * i + 1] = c.y;
+                cc[3 * i + 2] = c.z;
+            }
+        });
+        int rc = device_build_bvh(s, prm.num_buckets, prm.max_prims_in_node,
+                                  static_cast<int>(prm.build_device) - 1, bx, cc);
+        if (rc) return rc;
     } else {
         if (prm.num_buckets < 2) return fail(CRT_E_INVALID, "num_buckets must be >= 2");
         Builder b(s->prims, s->order, prm.num_buckets, prm.max_prims_in_node);
@@ -384,31 +450,54 @@ static void stage(crt_scene* s) {
         d.axis = n.axis;
         d.flags = n.flags;
     }
-    s->refs.resize(s->order.size());
-    s->spheres.clear();
-    s->sphere_mat.clear();
-    s->quads.clear();
-    s->quad_mat.clear();
-    for (size_t slot = 0; slot < s->order.size(); ++slot) {
-        const Prim& p = s->prims[s->order[slot]];
-        if (p.kind == CRT_SPHERE) {
-            s->refs[slot] = static_cast<uint32_t>(s->spheres.size());
-            DevSphere d;
-            d.c[0] = p.v[0]; d.c[1] = p.v[1]; d.c[2] = p.v[2]; d.r = p.v[3];
-            s->spheres.push_back(d);
-            s->sphere_mat.push_back(p.material);
-        } else {
-            s->refs[slot] = kRefQuad | static_cast<uint32_t>(s->quads.size());
-            DevQuad q{};
-            std::memcpy(q.v, p.v + 0, 3 * sizeof(double));
-            std::memcpy(q.s1, p.v + 3, 3 * sizeof(double));
-            std::memcpy(q.s2, p.v + 6, 3 * sizeof(double));
-            std::memcpy(q.n, p.v + 9, 3 * sizeof(double));
-            std::memcpy(q.sn, p.v + 12, 3 * sizeof(double));
-            s->quads.push_back(q);
-            s->quad_mat.push_back(p.material);
+    // slot arrays: per chunk of slots count the spheres, then fill at prefix offsets (the sphere /
+    // parallelogram arrays are in slot order either way)
+    const size_t ns = s->order.size();
+    s->refs.resize(ns);
+    constexpr size_t kChunk = 1 << 16;
+    const size_t nchunks = (ns + kChunk - 1) / kChunk;
+    std::vector<size_t> csph(nchunks + 1, 0), cquad(nchunks + 1, 0);
+    parallel_for(nchunks, 1, [&](size_t a, size_t b) {
+        for (size_t c = a; c < b; ++c) {
+            size_t k = 0;
+            for (size_t slot = c * kChunk; slot < std::min(ns, (c + 1) * kChunk); ++slot)
+                k += s->prims[s->order[slot]].kind == CRT_SPHERE;
+            csph[c + 1] = k;
+            cquad[c + 1] = std::min(ns, (c + 1) * kChunk) - c * kChunk - k;
         }
+    });
+    for (size_t c = 0; c < nchunks; ++c) {
+        csph[c + 1] += csph[c];
+        cquad[c + 1] += cquad[c];
     }
+    s->spheres.resize(csph[nchunks]);
+    s->sphere_mat.resize(csph[nchunks]);
+    s->quads.resize(cquad[nchunks]);
+    s->quad_mat.resize(cquad[nchunks]);
+    parallel_for(nchunks, 1, [&](size_t a, size_t b) {
+        for (size_t c = a; c < b; ++c) {
+            size_t is = csph[c], iq = cquad[c];
+            for (size_t slot = c * kChunk; slot < std::min(ns, (c + 1) * kChunk); ++slot) {
+                const Prim& p = s->prims[s->order[slot]];
+                if (p.kind == CRT_SPHERE) {
+                    s->refs[slot] = static_cast<uint32_t>(is);
+                    DevSphere& d = s->spheres[is];
+                    d.c[0] = p.v[0]; d.c[1] = p.v[1]; d.c[2] = p.v[2]; d.r = p.v[3];
+                    s->sphere_mat[is++] = p.material;
+                } else {
+                    s->refs[slot] = kRefQuad | static_cast<uint32_t>(iq);
+                    DevQuad& q = s->quads[iq];
+                    q = DevQuad{};
+                    std::memcpy(q.v, p.v + 0, 3 * sizeof(double));
+                    std::memcpy(q.s1, p.v + 3, 3 * sizeof(double));
+                    std::memcpy(q.s2, p.v + 6, 3 * sizeof(double));
+                    std::memcpy(q.n, p.v + 9, 3 * sizeof(double));
+                    std::memcpy(q.sn, p.v + 12, 3 * sizeof(double));
+                    s->quad_mat[iq++] = p.material;
+                }
+            }
+        }
+    });
     s->dmats.resize(s->materials.size());
     for (size_t i = 0; i < s->materials.size(); ++i) {
         const crt_material& m = s->materials[i];
@@ -517,7 +606,7 @@ struct SceneOut {
         return static_cast<uint32_t>(mats.size() - 1);
     }
     uint32_t lambertian(V3 c) { return mat(CRT_LAMBERTIAN, c, 0); }
-    uint32_t metal(V3 c, double fuzz) { return mat(CRT_METAL, c, std::fmin(fuzz, 1.)); }
+    uint32_t metal(V3 c, double fuzz) { return mat(CRT_METAL, c, gfmin(fuzz, 1.)); }
     uint32_t dielectric(double ri) { return mat(CRT_DIELECTRIC, {0, 0, 0}, ri); }
     uint32_t light(V3 c, double k) { return mat(CRT_DIFFUSE_LIGHT, c, k); }
     void sphere(V3 c, double r, uint32_t m) {

@@ -115,6 +115,8 @@ int device_render(const crt_scene* s, int device, const crt_camera* cam, const c
 int device_closest_hits(crt_scene* s, int device, const double* rays, size_t n, double t_min,
                         double t_max, crt_hit* out);
 int device_count(int* n);
+int device_build_bvh(crt_scene* s, uint32_t num_buckets, uint32_t max_leaf, int device,
+                     const std::vector<double>& boxes, const std::vector<double>& cents);
 int device_ppm_values(int device, const double* d_rgb, size_t n, int32_t* h_values, void* stream);
 // host: RGB::as_string's three integers for one pixel (std::pow, x86 int conversion)
 void ppm_pixel_host(const double rgb[3], int32_t out[3]);

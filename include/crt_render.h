@@ -72,7 +72,7 @@ typedef struct crt_bvh_params {
     uint32_t num_buckets;
     uint32_t max_prims_in_node;
     uint32_t linear;
-    uint32_t reserved;
+    uint32_t build_device;  /* 0: build on the host; d + 1: build on GPU d (the same tree) */
 } crt_bvh_params;
 
 /* ---- camera ---------------------------------------------------------------------------- */

@@ -96,6 +96,54 @@ def ppm_edge_frame() -> np.ndarray:
     return f
 
 
+def tie_scene(seed: int, n: int) -> crt.SceneData:
+    """A random scene of spheres, parallelograms and boxes on a 0.1 grid with ~10% signed-zero
+    coordinates: many equal bounds and centroids, so the BVH folds and partitions see ties."""
+    from cpp_raytracer_amd import CRT_BOX, CRT_PARALLELOGRAM, CRT_SPHERE, MATERIAL_DTYPE, OBJECT_DTYPE
+    rng = np.random.default_rng(seed)
+    d = crt.SceneData.named("config1")
+    mats = np.zeros(2, MATERIAL_DTYPE)
+    mats["kind"] = 1
+    mats["color"] = 0.5
+    objs = np.zeros(n, OBJECT_DTYPE)
+    kinds = rng.choice([CRT_SPHERE, CRT_PARALLELOGRAM, CRT_BOX], n, p=[0.6, 0.3, 0.1])
+    objs["kind"] = kinds
+    objs["material"] = rng.integers(0, 2, n)
+    v = np.round(rng.normal(0, 3, (n, 9)), 1)
+    v[rng.random((n, 9)) < 0.1] = -0.0
+    v[kinds == CRT_SPHERE, 3] = np.abs(v[kinds == CRT_SPHERE, 3]) + 0.1
+    box = kinds == CRT_BOX
+    v[box, 3:6] = v[box, 0:3] + np.abs(v[box, 3:6]) + 0.5
+    objs["v"] = v
+    d.materials, d.objects = mats, objs
+    return d
+
+
+def gen_bvh_ties(tmp: Path) -> None:
+    """The reference's BVH (oracle/_ref bvh mode) of tie-heavy random scenes."""
+    out = {}
+    for seed, n in TIE_CASES:
+        d = tie_scene(seed, n)
+        p = tmp / f"ties{seed}.crts"
+        d.save(p)
+        run("bvh", p, tmp / "t.bin")
+        b = (tmp / "t.bin").read_bytes()
+        nn, npr = np.frombuffer(b, "<u8", 2)
+        nodes = np.frombuffer(b, crt.NODE_DTYPE, int(nn), 16)
+        k = f"s{seed}_"
+        out[k + "objects"] = d.objects
+        out[k + "materials"] = d.materials
+        out[k + "bounds"] = nodes["bounds"]
+        out[k + "index"] = nodes["index"]
+        out[k + "count"] = nodes["count"]
+        out[k + "axis"] = nodes["axis"]
+        out[k + "order"] = np.frombuffer(b, "<u4", int(npr), 16 + 64 * int(nn))
+    np.savez_compressed(GOLD / "bvh_ties.npz", **out)
+
+
+TIE_CASES = [(4, 100), (5, 3000), (7, 20000)]
+
+
 def gen_ppm(tmp: Path) -> None:
     """Image::send_as_ppm integers (oracle/_ref ppm mode) for the config-1 golden render and the
     edge frame."""
@@ -176,14 +224,15 @@ def main() -> None:
             run("hits", p, rays_path, out)
             np.savez_compressed(GOLD / f"hits_{name}.npz", rays=rays, hits=np.load(out))
         gen_ppm(tmp)
+        gen_bvh_ties(tmp)
     (GOLD / "golden.json").write_text(json.dumps(meta, indent=1, sort_keys=True))
     print("golden fixtures written to", GOLD)
 
 
 if __name__ == "__main__":
-    if sys.argv[1:] == ["ppm"]:  # only the PPM-value fixtures
+    if sys.argv[1:] in (["ppm"], ["ties"]):  # only the PPM-value / tie-BVH fixtures
         subprocess.run(["make", "-C", str(ROOT / "oracle"), "ref"], check=True)
         with tempfile.TemporaryDirectory() as td:
-            gen_ppm(Path(td))
+            (gen_ppm if sys.argv[1] == "ppm" else gen_bvh_ties)(Path(td))
     else:
         main()

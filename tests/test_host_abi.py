@@ -158,3 +158,21 @@ def test_render_without_gpu_fails_loudly(crt):
     cam = crt.resolve_camera(s.data.camera, 1)
     with pytest.raises(crt.CrtError, match="no HIP device|no CPU fallback"):
         s.render(cam)
+
+
+@pytest.mark.parametrize("seed", [4, 5, 7])
+def test_bvh_ties_match_reference(crt, seed):
+    """Tie-heavy random scenes (0.1-grid coordinates, signed zeros): the host build equals the
+    reference's BVH bit for bit (std::fmin/fmax keep glibc's tie rule: fmin(+0, -0) = -0)."""
+    import sys
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import crt_oracle_py as orc
+    g = load_npz("bvh_ties.npz")
+    k = f"s{seed}_"
+    d = crt.SceneData.named("config1")
+    d.materials, d.objects = g[k + "materials"], g[k + "objects"]
+    for nodes, order in (crt.GpuScene(d).export_bvh(), orc.bvh(d)):
+        assert np.array_equal(nodes["bounds"].view(np.uint64), g[k + "bounds"].view(np.uint64))
+        for f in ("index", "count", "axis"):
+            assert np.array_equal(nodes[f], g[k + f])
+        assert np.array_equal(order, g[k + "order"])
