@@ -86,7 +86,11 @@ public:
     std::vector<crt_object> object_records;
     GpuScene(const Hittable& world, uint32_t num_buckets, uint32_t max_prims, bool linear) {
         Flat f(world);
-        crt_bvh_params p{num_buckets, max_prims, linear ? 1u : 0u, 0};
+        // the tree is the reference's either way; with a GPU visible it is built on device 0
+        // (crt_bvh_params.build_device), above 100k primitives where that pays
+        int ndev = 0;
+        const uint32_t on_gpu = (!linear && f.objects.size() > 100000 && crt_device_count(&ndev) == 0 && ndev > 0) ? 1u : 0u;
+        crt_bvh_params p{num_buckets, max_prims, linear ? 1u : 0u, on_gpu};
         if (crt_scene_create(f.materials.data(), f.materials.size(), f.objects.data(), f.objects.size(), &p, &s))
             die("crt_scene_create");
         materials = std::move(f.material_ptrs);
