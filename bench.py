@@ -33,6 +33,11 @@ sys.path.insert(0, str(ROOT))
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 FP64_VECTOR_PEAK_TFLOPS = 78.6  # MI355X spec (vector FP64)
 NODE_B, SPHERE_B, QUAD_B, PIXEL_B = 56, 36, 124, 24
+SCENE_DATA = {
+    "rtow_final": "synthetic: rtweekend_final_image scene built by the reference's RNG at set_seed(42)",
+    "cornell": "synthetic: cornell_box_test(false) scene of the reference's src/main.cpp (no randomness)",
+    "millions": "synthetic: millions_of_spheres scene built by the reference's RNG at set_seed(42)",
+}
 
 
 def parse():
@@ -114,7 +119,7 @@ def main():
     data = crt.SceneData.named(args.scene, args.seed)
     data.camera = camera_with(data.camera, image_w=args.width, image_h=args.height,
                               samples_per_pixel=args.spp, max_depth=args.depth)
-    scene = crt.GpuScene(data)
+    scene = crt.GpuScene(data, build_device=local if len(data.objects) > 100000 else None)
     info = scene.info()
     scene.upload(local)
     cam = crt.resolve_camera(data.camera, args.base_seed)
@@ -195,7 +200,7 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic: rtweekend_final_image scene built by the reference's RNG at set_seed(42)",
+            "data": SCENE_DATA.get(args.scene, f"synthetic: {args.scene} scene of the reference's src/main.cpp"),
             "config": {"workload": f"{args.scene} seed {args.seed}, {w}x{h}, {args.spp} spp, max_depth {args.depth}"
                                    f" (BASELINE config 2)" if (args.scene, w, h, args.spp, args.depth) ==
                                    ("rtow_final", 1200, 800, 500, 50) else
