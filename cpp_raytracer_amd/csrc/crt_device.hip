@@ -74,6 +74,13 @@ struct Counters {
     unsigned long long it_walk, it_leaf, it_shade;  // wave iterations (lane utilization)
 };
 
+// one lane's counts in the instrumented pass (32-bit: a lane handles one sample chunk), added to
+// the 64-bit Counters at the end
+struct LaneCounters {
+    uint32_t rays, nodes, sphere_tests, quad_tests;
+    uint32_t it_walk, it_leaf, it_shade;
+};
+
 // counts one per wave: only the lowest active lane increments
 __device__ __forceinline__ bool wave_leader() {
     const uint64_t m = __ballot(1);
@@ -314,7 +321,7 @@ struct Stack {
 template <typename SE, bool COUNT>
 __device__ __forceinline__ bool trace(const SceneView& S, Stack<SE>& st, const double o[3],
                                       const double d[3], double tmin, double& tmax,
-                                      uint32_t& hit_ref, Counters& ctr) {
+                                      uint32_t& hit_ref, LaneCounters& ctr) {
     const double inv[3] = {1 / d[0], 1 / d[1], 1 / d[2]};
     const uint32_t neg = (d[0] < 0 ? 1u : 0u) | (d[1] < 0 ? 2u : 0u) | (d[2] < 0 ? 4u : 0u);
     const double a = d[0] * d[0] + d[1] * d[1] + d[2] * d[2];  // dot(ray.dir, ray.dir)
@@ -429,7 +436,7 @@ __device__ __forceinline__ void trav_init(const double o[3], const double d[3], 
 // with per-lane bound addresses x[neg] / x[!neg].
 template <typename SE, bool COUNT, bool EXACT>
 __device__ __forceinline__ void walk(const SceneView& S, Stack<SE>& st, const double o[3],
-                                     double tmin, Trav& R, Counters& ctr) {
+                                     double tmin, Trav& R, LaneCounters& ctr) {
     uint32_t cur = R.cur, sp = R.sp;
     while (true) {
         const uint4 meta = reinterpret_cast<const uint4*>(S.nodes + cur)[3];  // index count axis flags
@@ -496,7 +503,7 @@ __device__ __forceinline__ void walk(const SceneView& S, Stack<SE>& st, const do
 template <typename SE, bool COUNT>
 __device__ __forceinline__ void leaf_step(const SceneView& S, Stack<SE>& st, const double o[3],
                                           const double d[3], double tmin, bool sphere_only,
-                                          Trav& R, Counters& ctr) {
+                                          Trav& R, LaneCounters& ctr) {
     const uint2 range = reinterpret_cast<const uint2*>(S.nodes + R.cur)[6];  // index, count
     const uint32_t end = range.x + range.y;
     const double ia = recip_a(R.a), lo = lim_tmin(tmin, R.a);
@@ -610,31 +617,32 @@ __device__ __forceinline__ bool shade(const SceneView& S, const CamView& C, Path
     const uint32_t mi = hit_record(S, ref, P.o, P.d, t, p, n, front);
     const DevMaterial& M = S.mats[mi];
     const uint32_t kind = M.kind;
-    double nd[3];
-    if (kind == CRT_LAMBERTIAN) {  // material.h:64-86
-        double rx, ry, rz;
-        random_unit_vector(P.rng, rx, ry, rz);
-        nd[0] = n[0] + rx; nd[1] = n[1] + ry; nd[2] = n[2] + rz;
-        if (fabs(nd[0]) < 1e-8 && fabs(nd[1]) < 1e-8 && fabs(nd[2]) < 1e-8) {
-            nd[0] = n[0]; nd[1] = n[1]; nd[2] = n[2];
-        }
-    } else if (kind == CRT_METAL) {  // material.h:116-139
+    const bool lam = kind == CRT_LAMBERTIAN, met = kind == CRT_METAL, die = kind == CRT_DIELECTRIC;
+    if (!(lam || met || die)) {  // DiffuseLight: emits, never scatters (material.h:248-263)
+        acc[0] = acc[0] + P.T[0] * M.emit[0];
+        acc[1] = acc[1] + P.T[1] * M.emit[1];
+        acc[2] = acc[2] + P.T[2] * M.emit[2];
+        return true;
+    }
+    // The scatter functions are interleaved by their common steps, so a wave with several
+    // materials runs each step once: unit(d) (Metal material.h:120, Dielectric :191), the
+    // Dielectric reflect-or-refract draw, random_unit_vector (Lambertian :70, Metal :123 — the
+    // only draw of either), then the reflection (vec3d.h:144-155) shared by Metal and a
+    // reflecting Dielectric. Every lane still makes its own material's draws in the reference's
+    // order (no lane draws in two of these steps).
+    double ux0 = 0, uy0 = 0, uz0 = 0;
+    if (met || die) {
         const double il = 1 / sqrt(P.d[0] * P.d[0] + P.d[1] * P.d[1] + P.d[2] * P.d[2]);
-        const double ux0 = P.d[0] * il, uy0 = P.d[1] * il, uz0 = P.d[2] * il;
-        const double k2 = 2 * (ux0 * n[0] + uy0 * n[1] + uz0 * n[2]);
-        double rx, ry, rz;
-        random_unit_vector(P.rng, rx, ry, rz);
-        nd[0] = (ux0 - n[0] * k2) + rx * M.param;
-        nd[1] = (uy0 - n[1] * k2) + ry * M.param;
-        nd[2] = (uz0 - n[2] * k2) + rz * M.param;
-        if (n[0] * nd[0] + n[1] * nd[1] + n[2] * nd[2] < 0) return true;  // absorbed; emits 0
-    } else if (kind == CRT_DIELECTRIC) {  // material.h:185-218, vec3d.h:144-200
-        const double ratio = front ? 1. / M.param : M.param / 1.;
-        const double il = 1 / sqrt(P.d[0] * P.d[0] + P.d[1] * P.d[1] + P.d[2] * P.d[2]);
-        const double ux0 = P.d[0] * il, uy0 = P.d[1] * il, uz0 = P.d[2] * il;
-        const double cosv = fmin((-ux0) * n[0] + (-uy0) * n[1] + (-uz0) * n[2], 1.);
+        ux0 = P.d[0] * il;
+        uy0 = P.d[1] * il;
+        uz0 = P.d[2] * il;
+    }
+    bool reflect = met;
+    double cosv = 0, ratio = 0;
+    if (die) {  // material.h:185-218, vec3d.h:168-200
+        ratio = front ? 1. / M.param : M.param / 1.;
+        cosv = fmin((-ux0) * n[0] + (-uy0) * n[1] + (-uz0) * n[2], 1.);
         const double sinv = sqrt(1 - cosv * cosv);
-        bool reflect;
         if (ratio * sinv > 1) {
             reflect = true;  // total internal reflection, no draw
         } else {
@@ -643,25 +651,34 @@ __device__ __forceinline__ bool shade(const SceneView& S, const CamView& C, Path
             const double refl = r0 + (1 - r0) * pow5(1 - cosv);
             reflect = rnd(P.rng, 0, 1) < refl;
         }
-        if (reflect) {
-            const double k2 = 2 * (ux0 * n[0] + uy0 * n[1] + uz0 * n[2]);
-            nd[0] = ux0 - n[0] * k2;
-            nd[1] = uy0 - n[1] * k2;
-            nd[2] = uz0 - n[2] * k2;
-        } else {
-            const double px = (ux0 + n[0] * cosv) * ratio;
-            const double py = (uy0 + n[1] * cosv) * ratio;
-            const double pz = (uz0 + n[2] * cosv) * ratio;
-            const double s = -sqrt(fabs(1 - (px * px + py * py + pz * pz)));
-            nd[0] = px + n[0] * s;
-            nd[1] = py + n[1] * s;
-            nd[2] = pz + n[2] * s;
+    }
+    double rx = 0, ry = 0, rz = 0;
+    if (lam || met) random_unit_vector(P.rng, rx, ry, rz);
+    double nd[3];
+    if (reflect) {  // Metal (material.h:116-139) or a reflecting Dielectric
+        const double k2 = 2 * (ux0 * n[0] + uy0 * n[1] + uz0 * n[2]);
+        nd[0] = ux0 - n[0] * k2;
+        nd[1] = uy0 - n[1] * k2;
+        nd[2] = uz0 - n[2] * k2;
+        if (met) {
+            nd[0] = nd[0] + rx * M.param;
+            nd[1] = nd[1] + ry * M.param;
+            nd[2] = nd[2] + rz * M.param;
+            if (n[0] * nd[0] + n[1] * nd[1] + n[2] * nd[2] < 0) return true;  // absorbed; emits 0
         }
-    } else {  // DiffuseLight: emits, never scatters (material.h:248-263)
-        acc[0] = acc[0] + P.T[0] * M.emit[0];
-        acc[1] = acc[1] + P.T[1] * M.emit[1];
-        acc[2] = acc[2] + P.T[2] * M.emit[2];
-        return true;
+    } else if (die) {  // refraction
+        const double px = (ux0 + n[0] * cosv) * ratio;
+        const double py = (uy0 + n[1] * cosv) * ratio;
+        const double pz = (uz0 + n[2] * cosv) * ratio;
+        const double sq = -sqrt(fabs(1 - (px * px + py * py + pz * pz)));
+        nd[0] = px + n[0] * sq;
+        nd[1] = py + n[1] * sq;
+        nd[2] = pz + n[2] * sq;
+    } else {  // Lambertian (material.h:64-86)
+        nd[0] = n[0] + rx; nd[1] = n[1] + ry; nd[2] = n[2] + rz;
+        if (fabs(nd[0]) < 1e-8 && fabs(nd[1]) < 1e-8 && fabs(nd[2]) < 1e-8) {
+            nd[0] = n[0]; nd[1] = n[1]; nd[2] = n[2];
+        }
     }
     if (kind != CRT_DIELECTRIC) {  // attenuation = intrinsic colour (dielectric: 1)
         P.T[0] = P.T[0] * M.color[0];
@@ -719,7 +736,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRT_WAVE
     const uint64_t wave = (static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x) >> 6;
     const uint32_t chunk = static_cast<uint32_t>(wave / W.tiles);
     const uint32_t tile = static_cast<uint32_t>(wave % W.tiles);
-    Counters ctr{};
+    LaneCounters ctr{};
     const unsigned long long t_start = COUNT ? wall_clock64() : 0;
     const uint32_t tx = tile % W.tiles_x, ty = tile / W.tiles_x;
     const uint32_t col = tx * 8 + (lane & 7);
@@ -747,21 +764,21 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRT_WAVE
         trav_init(P.o, P.d, R);
         if (COUNT) ctr.rays++;
     }
-    unsigned long long cw = 0, cl = 0, cs = 0;
+    uint32_t cw = 0, cl = 0, cs = 0;  // wall_clock64 ticks (100 MHz), differences mod 2^32
     while (true) {
         // traversal rounds (walk to the next entered leaf, test it) until enough lanes hold a
         // finished ray, or none is traversing
         while (true) {
-            if (COUNT) cw -= wall_clock64();
+            if (COUNT) cw -= static_cast<uint32_t>(wall_clock64());
             if (!W.exact_slab && __ballot(R.state == kWalk && (R.neg & kZeroDir)) == 0) {
                 if (R.state == kWalk) walk<SE, COUNT, false>(S, st, P.o, C.t_min, R, ctr);
             } else {
                 if (R.state == kWalk) walk<SE, COUNT, true>(S, st, P.o, C.t_min, R, ctr);
             }
-            if (COUNT) cw += wall_clock64();
-            if (COUNT) cl -= wall_clock64();
+            if (COUNT) cw += static_cast<uint32_t>(wall_clock64());
+            if (COUNT) cl -= static_cast<uint32_t>(wall_clock64());
             if (R.state == kLeaf) leaf_step<SE, COUNT>(S, st, P.o, P.d, C.t_min, W.sphere_only != 0, R, ctr);
-            if (COUNT) cl += wall_clock64();
+            if (COUNT) cl += static_cast<uint32_t>(wall_clock64());
             const uint64_t pending = __ballot(R.state == kWalk);
             const uint64_t finished = __ballot(R.state == kDone);
             if (pending == 0 || __popcll(finished) >= kShadeBatch) break;
@@ -769,7 +786,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRT_WAVE
         const uint64_t m_done = __ballot(R.state == kDone);
         if (m_done == 0) break;  // every lane idle: the chunk is finished
         {
-            if (COUNT) cs -= wall_clock64();
+            if (COUNT) cs -= static_cast<uint32_t>(wall_clock64());
             if (R.state == kDone) {
                 if (COUNT && wave_leader()) ctr.it_shade++;
                 bool ended = shade(S, C, P, R.found, R.ref, R.tmax, acc);
@@ -784,13 +801,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRT_WAVE
                     if (COUNT) ctr.rays++;
                 }
             }
-            if (COUNT) cs += wall_clock64();
+            if (COUNT) cs += static_cast<uint32_t>(wall_clock64());
         }
-    }
-    if (COUNT) {
-        ctr.cyc_walk = cw;
-        ctr.cyc_leaf = cl;
-        ctr.cyc_shade = cs;
     }
     if (valid && !COUNT) {
         const size_t owned_pixel = static_cast<size_t>(k) * C.w + col;
@@ -800,20 +812,21 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRT_WAVE
         dst[2] = acc[2];
     }
     if (COUNT) {
-        atomicAdd(&counters->rays, ctr.rays);
-        atomicAdd(&counters->nodes, ctr.nodes);
-        atomicAdd(&counters->sphere_tests, ctr.sphere_tests);
-        atomicAdd(&counters->quad_tests, ctr.quad_tests);
+        using ull = unsigned long long;
+        atomicAdd(&counters->rays, static_cast<ull>(ctr.rays));
+        atomicAdd(&counters->nodes, static_cast<ull>(ctr.nodes));
+        atomicAdd(&counters->sphere_tests, static_cast<ull>(ctr.sphere_tests));
+        atomicAdd(&counters->quad_tests, static_cast<ull>(ctr.quad_tests));
         if (lane == 0) {  // per-wave phase times (the wave executes each phase as one)
-            atomicAdd(&counters->cyc_walk, ctr.cyc_walk);
-            atomicAdd(&counters->cyc_leaf, ctr.cyc_leaf);
-            atomicAdd(&counters->cyc_shade, ctr.cyc_shade);
+            atomicAdd(&counters->cyc_walk, static_cast<ull>(cw));
+            atomicAdd(&counters->cyc_leaf, static_cast<ull>(cl));
+            atomicAdd(&counters->cyc_shade, static_cast<ull>(cs));
             atomicAdd(&counters->cyc_total, wall_clock64() - t_start);
         }
         // iteration counters are incremented by whichever lane led that iteration
-        atomicAdd(&counters->it_walk, ctr.it_walk);
-        atomicAdd(&counters->it_leaf, ctr.it_leaf);
-        atomicAdd(&counters->it_shade, ctr.it_shade);
+        atomicAdd(&counters->it_walk, static_cast<ull>(ctr.it_walk));
+        atomicAdd(&counters->it_leaf, static_cast<ull>(ctr.it_leaf));
+        atomicAdd(&counters->it_shade, static_cast<ull>(ctr.it_shade));
     }
 }
 
@@ -891,7 +904,7 @@ __global__ __launch_bounds__(kBlock) void hits_kernel(SceneView S, const double*
     double d[3] = {rays[6 * i + 3], rays[6 * i + 4], rays[6 * i + 5]};
     double tmax = t_max;
     uint32_t ref = 0;
-    Counters ctr{};
+    LaneCounters ctr{};
     crt_hit h{};
     h.prim = -1;
     if (trace<uint32_t, false>(S, st, o, d, t_min, tmax, ref, ctr)) {
