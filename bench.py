@@ -3,7 +3,7 @@
 
 One step = one whole frame of BASELINE config 2 (rtweekend_final_image scene at set_seed(42),
 1200x800, 500 spp, max_depth 50) rendered by the gfx950 kernel from a scene already resident in
-HBM. With N ranks (torchrun, one process per GPU) the frame's rows are dealt to ranks in 16-row
+HBM. With N ranks (torchrun, one process per GPU) the frame's rows are dealt to ranks in 4-row
 blocks, each rank renders its blocks, and the tiles are all-gathered over RCCL (xGMI) into a full
 frame on every rank: the total work is fixed, so scaling is "strong".
 
@@ -107,9 +107,16 @@ def main():
     if world != args.gpus:
         args.gpus = world if world > 1 else args.gpus
     distributed = world > 1
+    # one GPU per rank; CRT_BENCH_BACKEND=gloo + ranks sharing a device rehearses the N>1 path
+    # on a one-GPU box (RCCL refuses two ranks on one device)
+    backend = os.environ.get("CRT_BENCH_BACKEND", "nccl")
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     if distributed:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
 
     def log(msg):
         if rank == 0:
@@ -124,7 +131,7 @@ def main():
     scene.upload(local)
     cam = crt.resolve_camera(data.camera, args.base_seed)
     h, w = args.height, args.width
-    rb = 16
+    rb = 4  # 4-row blocks: 800 rows deal exactly over 1, 2, 4, 8 ranks (16 left 7 vs 6 at N=8)
     tiling = Tiling(rb, world, rank, 0)
     owned = owned_rows(h, rb, world, rank)
     log(f"scene {args.scene}: {info.num_primitives} prims, {info.num_nodes} nodes, depth {info.depth}, "
@@ -206,7 +213,7 @@ def main():
                                    ("rtow_final", 1200, 800, 500, 50) else
                                    f"{args.scene} seed {args.seed}, {w}x{h}, {args.spp} spp, max_depth {args.depth}",
                        "samples_per_step": h * w * args.spp, "primitives": int(info.num_primitives),
-                       "bvh_nodes": int(info.num_nodes), "partition": f"16-row blocks over {world} ranks, "
+                       "bvh_nodes": int(info.num_nodes), "partition": f"{rb}-row blocks over {world} ranks, "
                        "RCCL all-gather of tiles" if distributed else "whole frame on one GPU"},
             "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved_gbs / HBM_PEAK_GBS, 4), "traffic": traffic,

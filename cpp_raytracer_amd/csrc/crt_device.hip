@@ -34,7 +34,11 @@ namespace dev {
 #ifndef CRT_BLOCK
 #define CRT_BLOCK 256
 #endif
-constexpr int kBlock = CRT_BLOCK;     // waves of 64; each wave starts on one 8x8 pixel tile
+#ifndef CRT_WALK_TAIL
+#define CRT_WALK_TAIL 0
+#endif
+constexpr int kBlock = CRT_BLOCK;
+constexpr int kWalkTail = CRT_WALK_TAIL;  // see walk()     // waves of 64; each wave starts on one 8x8 pixel tile
 constexpr double kScale = 1 / static_cast<double>(4294967295u - 1);  // rand_util.h:110-112
 
 struct SceneView {
@@ -492,6 +496,9 @@ __device__ __forceinline__ void walk(const SceneView& S, Stack<SE>& st, const do
         }
         cur = inner ? near_child : top;
         sp = inner ? sp + 1 : sp - 1;
+        // once at most kWalkTail lanes still walk, they pause (state stays WALK) and the wave
+        // moves on to the leaf phase; they resume in the next round
+        if (kWalkTail > 0 && __popcll(__ballot(1)) <= kWalkTail) break;
     }
     R.cur = cur;
     R.sp = sp;
@@ -1306,7 +1313,7 @@ int render_multi(crt_scene* s, const crt_camera* cam, int num_devices, double* h
     std::vector<double*> bufs(num_devices, nullptr);
     std::vector<hipStream_t> streams(num_devices, nullptr);
     std::vector<hipEvent_t> ev0(num_devices, nullptr), ev1(num_devices, nullptr);
-    const uint32_t rb = 16;
+    const uint32_t rb = 4;  // 4-row blocks: 800 rows split exactly over 1, 2, 4, 8 devices
     int rc = CRT_OK;
     for (int d = 0; d < num_devices && rc == CRT_OK; ++d) {
         rc = device_upload(s, d);

@@ -1,6 +1,6 @@
 // Drop-in for the reference's base/camera.h. Same fluent setters and render() entry points;
 // render runs the per-pixel / per-sample loop on the MI355X GPUs of this process through the C ABI
-// (crt_render: rows dealt to every visible device in 16-row blocks, tiles gathered to the host).
+// (crt_render: rows dealt to every visible device in 4-row blocks, tiles gathered to the host).
 // There is no CPU fallback: without a GPU render prints the reason and exits, as the reference does
 // on its own errors.
 //
