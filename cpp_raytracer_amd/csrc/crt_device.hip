@@ -248,6 +248,20 @@ __device__ __forceinline__ bool hit_sphere(const DevSphere& sp, const double o[3
     return true;
 }
 
+// hit_sphere's cheap part only: false when the sphere provably cannot be accepted for any
+// t_max' <= the t_max behind `hi` (no real root, or both roots outside (t_min, t_max)).
+__device__ __forceinline__ bool sphere_candidate(const DevSphere& sp, const double o[3], const double d[3],
+                                                 double a, double lo, double hi) {
+    double ocx = o[0] - sp.c[0], ocy = o[1] - sp.c[1], ocz = o[2] - sp.c[2];
+    double b = d[0] * ocx + d[1] * ocy + d[2] * ocz;
+    double c = (ocx * ocx + ocy * ocy + ocz * ocz) - sp.r * sp.r;
+    double disc = b * b - a * c;
+    if (disc < 0) return false;
+    const double sqa = disc * __builtin_amdgcn_rsq(disc);
+    const double m = (fabs(b) + sqa) * 0x1p-12;
+    return !((-b - sqa) - m > hi || (-b + sqa) + m < lo);
+}
+
 // Parallelogram::hit_by (parallelogram.h:177-240)
 __device__ __forceinline__ bool hit_quad(const DevQuad& q, const double o[3], const double d[3],
                                          double tmin, double tmax, double& t) {
@@ -515,7 +529,35 @@ __device__ __forceinline__ void leaf_step(const SceneView& S, Stack<SE>& st, con
     const uint32_t end = range.x + range.y;
     const double ia = recip_a(R.a), lo = lim_tmin(tmin, R.a);
     double hi = lim_tmax(R.tmax, R.a);
-    if (sphere_only) {
+    if (sphere_only && range.y <= 32) {
+        // two passes: the cheap candidate test of every sphere against the leaf-entry t_max, then
+        // the full test of the candidates in slot order with the shrinking t_max. A sphere the
+        // first pass rejects is rejected by the full test for any smaller t_max too, so the hits
+        // and the tie order are the sequential loop's; the full-test pass runs only as often as
+        // the lane with most candidates needs (typically 1-3 of 6-12).
+        uint32_t cand = 0;
+        DevSphere cur = S.spheres[range.x];
+        for (uint32_t i = 0; i < range.y; ++i) {
+            const DevSphere nxt = S.spheres[range.x + i + 1];
+            if (COUNT) {
+                ctr.sphere_tests++;
+                if (wave_leader()) ctr.it_leaf++;
+            }
+            if (sphere_candidate(cur, o, d, R.a, lo, hi)) cand |= 1u << i;
+            cur = nxt;
+        }
+        while (cand) {
+            const uint32_t i = range.x + __builtin_ctz(cand);
+            cand &= cand - 1;
+            double t;
+            if (hit_sphere(S.spheres[i], o, d, R.a, ia, tmin, R.tmax, lo, hi, t)) {
+                R.tmax = t;
+                hi = lim_tmax(t, R.a);
+                R.ref = i;
+                R.found = true;
+            }
+        }
+    } else if (sphere_only) {
         DevSphere cur = S.spheres[range.x];
         for (uint32_t i = range.x; i < end; ++i) {
             // one past the leaf's last sphere is still inside the scene copy (sphere_mat follows
