@@ -652,16 +652,13 @@ __device__ __forceinline__ void start_path(const CamView& C, uint32_t row, uint3
 
 // One level of ray_color (camera.h:205-258) after the closest-hit query: scatters
 // (material.h:64-263) into the next ray, or ends the path adding T * (background | emission) to
-// acc (the lane's partial-sum slot in HBM; null in the instrumented pass). Returns true when the
-// path has ended (miss, light, absorption).
+// acc. Returns true when the path has ended (miss, light, absorption).
 __device__ __forceinline__ bool shade(const SceneView& S, const CamView& C, Path& P, bool hit,
-                                      uint32_t ref, double t, double* acc) {
+                                      uint32_t ref, double t, double acc[3]) {
     if (!hit) {
-        if (acc) {
-            acc[0] = acc[0] + P.T[0] * C.bg[0];
-            acc[1] = acc[1] + P.T[1] * C.bg[1];
-            acc[2] = acc[2] + P.T[2] * C.bg[2];
-        }
+        acc[0] = acc[0] + P.T[0] * C.bg[0];
+        acc[1] = acc[1] + P.T[1] * C.bg[1];
+        acc[2] = acc[2] + P.T[2] * C.bg[2];
         return true;
     }
     double p[3], n[3];
@@ -671,11 +668,9 @@ __device__ __forceinline__ bool shade(const SceneView& S, const CamView& C, Path
     const uint32_t kind = M.kind;
     const bool lam = kind == CRT_LAMBERTIAN, met = kind == CRT_METAL, die = kind == CRT_DIELECTRIC;
     if (!(lam || met || die)) {  // DiffuseLight: emits, never scatters (material.h:248-263)
-        if (acc) {
-            acc[0] = acc[0] + P.T[0] * M.emit[0];
-            acc[1] = acc[1] + P.T[1] * M.emit[1];
-            acc[2] = acc[2] + P.T[2] * M.emit[2];
-        }
+        acc[0] = acc[0] + P.T[0] * M.emit[0];
+        acc[1] = acc[1] + P.T[1] * M.emit[1];
+        acc[2] = acc[2] + P.T[2] * M.emit[2];
         return true;
     }
     // The scatter functions are interleaved by their common steps, so a wave with several
@@ -808,15 +803,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRT_WAVE
     const uint32_t pixel = row * C.w + col;
     uint32_t s = chunk * W.chunk_len;
     const uint32_t s_end = valid ? min(C.spp, s + W.chunk_len) : s;
-    // this lane's partial sum lives in its partial[chunk][pixel] slot (read-modify-write at each
-    // path end, in sample order), not in registers
-    double* acc = nullptr;
-    if (valid && !COUNT) {
-        acc = partial + (static_cast<size_t>(chunk) * W.owned_rows * C.w + static_cast<size_t>(k) * C.w + col) * 3;
-        acc[0] = 0;
-        acc[1] = 0;
-        acc[2] = 0;
-    }
+    double acc[3] = {0, 0, 0};
     Path P;
     Trav R;
     R.state = kIdle;
@@ -865,6 +852,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRT_WAVE
             }
             if (COUNT) cs += static_cast<uint32_t>(wall_clock64());
         }
+    }
+    if (valid && !COUNT) {
+        const size_t owned_pixel = static_cast<size_t>(k) * C.w + col;
+        double* dst = partial + (static_cast<size_t>(chunk) * W.owned_rows * C.w + owned_pixel) * 3;
+        dst[0] = acc[0];
+        dst[1] = acc[1];
+        dst[2] = acc[2];
     }
     if (COUNT) {
         using ull = unsigned long long;
