@@ -226,7 +226,7 @@ def main():
                      "nodes_per_ray": round(cnt.nodes_visited / max(1, cnt.rays), 3),
                      "prim_tests_per_ray": round((cnt.sphere_tests + cnt.parallelogram_tests) / max(1, cnt.rays), 3)},
             "wave_time_share": {k: round(getattr(cnt, "ticks_" + k) / max(1, cnt.ticks_total), 4)
-                                for k in ("walk", "leaf", "shade")},
+                                for k in ("walk", "leaf", "shade", "tail")},
             "lane_utilization": {
                 "walk": round(cnt.nodes_visited / max(1, 64 * cnt.wave_iters_walk), 4),
                 "leaf": round((cnt.sphere_tests + cnt.parallelogram_tests) / max(1, 64 * cnt.wave_iters_leaf), 4),

@@ -75,6 +75,7 @@ struct Work {
 struct Counters {
     unsigned long long rays, nodes, sphere_tests, quad_tests;
     unsigned long long cyc_walk, cyc_leaf, cyc_shade, cyc_total;  // wave cycles (instrumented pass)
+    unsigned long long cyc_tail;  // from the wave's first idle lane (chunk done) to its end
     unsigned long long it_walk, it_leaf, it_shade;  // wave iterations (lane utilization)
 };
 
@@ -814,6 +815,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRT_WAVE
         if (COUNT) ctr.rays++;
     }
     uint32_t cw = 0, cl = 0, cs = 0;  // wall_clock64 ticks (100 MHz), differences mod 2^32
+    unsigned long long t_first_idle = 0;
     while (true) {
         // traversal rounds (walk to the next entered leaf, test it) until enough lanes hold a
         // finished ray, or none is traversing
@@ -833,6 +835,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRT_WAVE
             if (pending == 0 || __popcll(finished) >= kShadeBatch) break;
         }
         const uint64_t m_done = __ballot(R.state == kDone);
+        if (COUNT && t_first_idle == 0 && __ballot(R.state == kIdle) != 0) t_first_idle = wall_clock64();
         if (m_done == 0) break;  // every lane idle: the chunk is finished
         {
             if (COUNT) cs -= static_cast<uint32_t>(wall_clock64());
@@ -870,7 +873,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRT_WAVE
             atomicAdd(&counters->cyc_walk, static_cast<ull>(cw));
             atomicAdd(&counters->cyc_leaf, static_cast<ull>(cl));
             atomicAdd(&counters->cyc_shade, static_cast<ull>(cs));
-            atomicAdd(&counters->cyc_total, wall_clock64() - t_start);
+            const unsigned long long t_end = wall_clock64();
+            atomicAdd(&counters->cyc_total, t_end - t_start);
+            atomicAdd(&counters->cyc_tail, t_first_idle ? t_end - t_first_idle : 0ull);
         }
         // iteration counters are incremented by whichever lane led that iteration
         atomicAdd(&counters->it_walk, static_cast<ull>(ctr.it_walk));
@@ -1114,7 +1119,10 @@ static int launch_render(const crt_scene* s, int device, const crt_camera* cam, 
     // the tiling / number of GPUs (bit-identical frames for 1..N devices). 64-sample chunks keep
     // ~8 chunks per pixel at BASELINE spp (enough threads for dynamic balance); at most 64 chunks.
     const uint32_t spp = cam->samples_per_pixel;
-    W.chunk_len = std::max<uint32_t>(64, (spp + 63) / 64);
+#ifndef CRT_CHUNK_MIN
+#define CRT_CHUNK_MIN 64
+#endif
+    W.chunk_len = std::max<uint32_t>(CRT_CHUNK_MIN, (spp + 63) / 64);
     W.chunks = (spp + W.chunk_len - 1) / W.chunk_len;
     const uint64_t waves = static_cast<uint64_t>(W.tiles) * W.chunks;
     const uint64_t blocks = (waves * 64 + dev::kBlock - 1) / dev::kBlock;
@@ -1182,6 +1190,7 @@ static int launch_render(const crt_scene* s, int device, const crt_camera* cam, 
         count_stats->wave_iters_walk = h.it_walk;
         count_stats->wave_iters_leaf = h.it_leaf;
         count_stats->wave_iters_shade = h.it_shade;
+        count_stats->ticks_tail = h.cyc_tail;
         if (std::getenv("CRT_DEBUG_COUNTERS"))
             std::fprintf(stderr, "crt counters: rays %llu nodes %llu sphere_tests %llu quad_tests %llu it_walk %llu "
                          "it_leaf %llu it_shade %llu\n", h.rays, h.nodes, h.sphere_tests, h.quad_tests, h.it_walk,

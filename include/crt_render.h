@@ -166,6 +166,7 @@ typedef struct crt_render_stats {
     /* wave iterations of each phase: lane utilization = lane work / (iterations * 64) with lane
      * work = nodes_visited, sphere+parallelogram tests, rays respectively */
     uint64_t wave_iters_walk, wave_iters_leaf, wave_iters_shade;
+    uint64_t ticks_tail;  /* summed per wave: ticks from its first idle lane to its end */
 } crt_render_stats;
 
 /* ---- entry points ---------------------------------------------------------------------- */
