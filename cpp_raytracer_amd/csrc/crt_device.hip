@@ -784,8 +784,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRT_WAVE
     }
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t wave = (static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x) >> 6;
-    const uint32_t chunk = static_cast<uint32_t>(wave / W.tiles);
-    const uint32_t tile = static_cast<uint32_t>(wave % W.tiles);
+    // tile-major: the chunks of one 8x8 tile are consecutive waves, so the four waves of a block
+    // share a tile, cost about the same and release the block's slot together
+    const uint32_t chunk = static_cast<uint32_t>(wave % W.chunks);
+    const uint32_t tile = static_cast<uint32_t>(wave / W.chunks);
     LaneCounters ctr{};
     const unsigned long long t_start = COUNT ? wall_clock64() : 0;
     const uint32_t tx = tile % W.tiles_x, ty = tile / W.tiles_x;
@@ -1116,11 +1118,13 @@ static int launch_render(const crt_scene* s, int device, const crt_camera* cam, 
     dev::Work W = w0;
     const uint64_t pixels = static_cast<uint64_t>(W.owned_rows) * cam->image_w;
     // Sample chunks: a function of spp ONLY, so every pixel's sum is grouped identically whatever
-    // the tiling / number of GPUs (bit-identical frames for 1..N devices). 64-sample chunks keep
-    // ~8 chunks per pixel at BASELINE spp (enough threads for dynamic balance); at most 64 chunks.
+    // the tiling / number of GPUs (bit-identical frames for 1..N devices). 24-sample chunks
+    // (21 per pixel at BASELINE spp, at most 64) keep waves short enough that 1/8 of a frame
+    // still spreads over ~8 rounds of resident waves (strong scaling), at 2% of the 1-GPU speed
+    // of 64-sample chunks.
     const uint32_t spp = cam->samples_per_pixel;
 #ifndef CRT_CHUNK_MIN
-#define CRT_CHUNK_MIN 64
+#define CRT_CHUNK_MIN 24
 #endif
     W.chunk_len = std::max<uint32_t>(CRT_CHUNK_MIN, (spp + 63) / 64);
     W.chunks = (spp + W.chunk_len - 1) / W.chunk_len;
