@@ -43,6 +43,8 @@ constexpr double kScale = 1 / static_cast<double>(4294967295u - 1);  // rand_uti
 
 struct SceneView {
     const DevNode* nodes;
+    const DevNode* top_nodes;  // LDS copy of the first ntop (breadth-first) nodes, HBM scenes
+    uint32_t ntop;
     const uint32_t* refs;
     const DevSphere* spheres;
     const uint32_t* sphere_mat;
@@ -70,6 +72,7 @@ struct Work {
     uint32_t bytes_nodes, bytes_refs, bytes_spheres, bytes_quads;
     uint32_t sphere_only;   // every primitive is a sphere: refs[slot] == slot
     uint32_t exact_slab;    // the scene needs walk_step's EXACT variant for every ray
+    uint32_t ntop;          // HBM-scene kernels: nodes [0, ntop) staged in LDS at lds_nodes
 };
 
 struct Counters {
@@ -355,19 +358,19 @@ __device__ __forceinline__ bool trace(const SceneView& S, Stack<SE>& st, const d
         while (true) {  // interior walk until a leaf is entered
             const NodeRegs n = load_node(S.nodes, cur);
             if (COUNT) ctr.nodes++;
-            const bool enter = slab(n, o, inv, neg, tmin, tmax) | ((n.flags & kNodeAlways) != 0);
+            const bool enter = slab(n, o, inv, neg, tmin, tmax) | (n.count > 0 && (n.flags & kNodeAlways) != 0);
             if (enter) {
                 if (n.count > 0) {
                     first = n.index;
                     count = n.count;
                     break;
                 }
-                if ((neg >> n.axis) & 1u) {
-                    st.put(sp++, cur + 1);
+                if ((neg >> n.axis) & 1u) {  // children: left = flags, right = index
+                    st.put(sp++, n.flags);
                     cur = n.index;
                 } else {
                     st.put(sp++, n.index);
-                    cur = cur + 1;
+                    cur = n.flags;
                 }
             } else {
                 if (sp == 0) {
@@ -453,12 +456,21 @@ __device__ __forceinline__ void trav_init(const double o[3], const double d[3], 
 // origin is not finite (R.neg & kZeroDir), and scenes with an inverted / NaN node box
 // (Work::exact_slab, where min/max would reorder the axis) take the EXACT variant, the reference's select sequence verbatim
 // with per-lane bound addresses x[neg] / x[!neg].
-template <typename SE, bool COUNT, bool EXACT>
+// node i of the breadth-first device array: with TOP, the first S.ntop nodes are read from their
+// LDS copy and the rest from HBM (generic loads); otherwise all from S.nodes
+template <bool TOP>
+__device__ __forceinline__ const DevNode* node_at(const SceneView& S, uint32_t i) {
+    if (TOP) return (i < S.ntop ? S.top_nodes : S.nodes) + i;
+    return S.nodes + i;
+}
+
+template <typename SE, bool COUNT, bool EXACT, bool TOP>
 __device__ __forceinline__ void walk(const SceneView& S, Stack<SE>& st, const double o[3],
                                      double tmin, Trav& R, LaneCounters& ctr) {
     uint32_t cur = R.cur, sp = R.sp;
     while (true) {
-        const uint4 meta = reinterpret_cast<const uint4*>(S.nodes + cur)[3];  // index count axis flags
+        const DevNode* np = node_at<TOP>(S, cur);
+        const uint4 meta = reinterpret_cast<const uint4*>(np)[3];  // index count axis flags
         const uint32_t top = st.get(sp > 0 ? static_cast<int>(sp) - 1 : 0);  // speculative pop
         if (COUNT) {
             ctr.nodes++;
@@ -468,7 +480,7 @@ __device__ __forceinline__ void walk(const SceneView& S, Stack<SE>& st, const do
         if (!EXACT) {
             // linear-mode nodes (kNodeAlways) carry [-inf, inf] bounds in the device copy: with
             // finite o and finite non-zero inv every slab is (-inf, inf), so they are entered
-            const double2* b = reinterpret_cast<const double2*>(S.nodes + cur);
+            const double2* b = reinterpret_cast<const double2*>(np);
             const double2 bx = b[0], by = b[1], bz = b[2];
             const double x0 = (bx.x - o[0]) * R.inv[0], x1 = (bx.y - o[0]) * R.inv[0];
             const double y0 = (by.x - o[1]) * R.inv[1], y1 = (by.y - o[1]) * R.inv[1];
@@ -477,7 +489,7 @@ __device__ __forceinline__ void walk(const SceneView& S, Stack<SE>& st, const do
             const double far = fmin(fmin(fmax(x0, x1), fmax(y0, y1)), fmax(z0, z1));
             enter = (near <= far) & (near < R.tmax) & (far > tmin);
         } else {
-            const double* b = reinterpret_cast<const double*>(S.nodes + cur);
+            const double* b = reinterpret_cast<const double*>(np);
             const uint32_t nx = R.neg & 1u, ny = (R.neg >> 1) & 1u, nz = (R.neg >> 2) & 1u;
             const double bx0 = b[0 + nx], bx1 = b[1 - nx];
             const double by0 = b[2 + ny], by1 = b[3 - ny];
@@ -494,7 +506,7 @@ __device__ __forceinline__ void walk(const SceneView& S, Stack<SE>& st, const do
             const bool c2 = !(xtmin > ztmax || ztmin > xtmax);
             if (ztmin > xtmin) xtmin = ztmin;
             if (ztmax < xtmax) xtmax = ztmax;
-            enter = (c1 & c2 & (xtmin < R.tmax) & (xtmax > tmin)) | ((meta.w & kNodeAlways) != 0);
+            enter = (c1 & c2 & (xtmin < R.tmax) & (xtmax > tmin)) | (meta.y != 0 && (meta.w & kNodeAlways) != 0);
         }
         // inner: descend to the near child, push the far one; missed: pop. The far child is
         // stored at level sp whatever the outcome (level sp is above the live stack unless it is
@@ -502,8 +514,8 @@ __device__ __forceinline__ void walk(const SceneView& S, Stack<SE>& st, const do
         // entered leaf (cur stays on it; leaf_step reads its primitive range) or an empty stack.
         const bool inner = enter && meta.y == 0;
         const bool far_first = (R.neg >> meta.z) & 1u;
-        const uint32_t near_child = far_first ? meta.x : cur + 1;
-        const uint32_t far_child = far_first ? cur + 1 : meta.x;
+        const uint32_t near_child = far_first ? meta.x : meta.w;  // children: left = flags, right = index
+        const uint32_t far_child = far_first ? meta.w : meta.x;
         st.put(static_cast<int>(sp), far_child);
         if (!inner && (enter || sp == 0)) {
             R.state = enter ? kLeaf : kDone;
@@ -522,11 +534,11 @@ __device__ __forceinline__ void walk(const SceneView& S, Stack<SE>& st, const do
 // the entered leaf's primitives in order (bvh.h:635-652), then "return" to the DFS.
 // Sphere-only scenes store spheres in slot order, so the slot indexes them directly and the next
 // sphere is loaded while the current one is tested.
-template <typename SE, bool COUNT>
+template <typename SE, bool COUNT, bool TOP>
 __device__ __forceinline__ void leaf_step(const SceneView& S, Stack<SE>& st, const double o[3],
                                           const double d[3], double tmin, bool sphere_only,
                                           Trav& R, LaneCounters& ctr) {
-    const uint2 range = reinterpret_cast<const uint2*>(S.nodes + R.cur)[6];  // index, count
+    const uint2 range = reinterpret_cast<const uint2*>(node_at<TOP>(S, R.cur))[6];  // index, count
     const uint32_t end = range.x + range.y;
     const double ia = recip_a(R.a), lo = lim_tmin(tmin, R.a);
     double hi = lim_tmax(R.tmax, R.a);
@@ -781,6 +793,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRT_WAVE
         S.spheres = reinterpret_cast<const DevSphere*>(smem + W.lds_spheres);
         S.quads = reinterpret_cast<const DevQuad*>(smem + W.lds_quads);
         __syncthreads();
+    } else if (W.ntop) {  // HBM scene: keep its top ntop nodes (breadth-first) in LDS
+        stage_lds(smem + W.lds_nodes, Sg.nodes, W.ntop * static_cast<uint32_t>(sizeof(DevNode)));
+        S.top_nodes = reinterpret_cast<const DevNode*>(smem + W.lds_nodes);
+        S.ntop = W.ntop;
+        __syncthreads();
     }
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t wave = (static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x) >> 6;
@@ -824,13 +841,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRT_WAVE
         while (true) {
             if (COUNT) cw -= static_cast<uint32_t>(wall_clock64());
             if (!W.exact_slab && __ballot(R.state == kWalk && (R.neg & kZeroDir)) == 0) {
-                if (R.state == kWalk) walk<SE, COUNT, false>(S, st, P.o, C.t_min, R, ctr);
+                if (R.state == kWalk) walk<SE, COUNT, false, !LSCENE>(S, st, P.o, C.t_min, R, ctr);
             } else {
-                if (R.state == kWalk) walk<SE, COUNT, true>(S, st, P.o, C.t_min, R, ctr);
+                if (R.state == kWalk) walk<SE, COUNT, true, !LSCENE>(S, st, P.o, C.t_min, R, ctr);
             }
             if (COUNT) cw += static_cast<uint32_t>(wall_clock64());
             if (COUNT) cl -= static_cast<uint32_t>(wall_clock64());
-            if (R.state == kLeaf) leaf_step<SE, COUNT>(S, st, P.o, P.d, C.t_min, W.sphere_only != 0, R, ctr);
+            if (R.state == kLeaf) leaf_step<SE, COUNT, !LSCENE>(S, st, P.o, P.d, C.t_min, W.sphere_only != 0, R, ctr);
             if (COUNT) cl += static_cast<uint32_t>(wall_clock64());
             const uint64_t pending = __ballot(R.state == kWalk);
             const uint64_t finished = __ballot(R.state == kDone);
@@ -983,7 +1000,7 @@ __global__ __launch_bounds__(kBlock) void hits_kernel(SceneView S, const double*
 // host launch plumbing
 
 static dev::SceneView view_of(const DeviceCopy& c) {
-    return dev::SceneView{c.nodes, c.refs, c.spheres, c.sphere_mat, c.quads, c.quad_mat, c.mats};
+    return dev::SceneView{c.nodes, nullptr, 0, c.refs, c.spheres, c.sphere_mat, c.quads, c.quad_mat, c.mats};
 }
 
 int device_count(int* n) {
@@ -1224,11 +1241,21 @@ static int dispatch_render(const crt_scene* s, int device, const crt_camera* cam
         W.lds_stack = W.lds_quads + W.bytes_quads;
         return launch_render<SE, false, true>(s, device, cam, W, scene_bytes + stack_bytes, d_rgb, st, count_stats);
     }
+    // HBM scene: the top of the (breadth-first) node array goes to LDS as far as it fits beside
+    // the stack without costing resident blocks (5 blocks of 4 waves, the VGPR limit, at
+    // <= 32 KB each)
+    const size_t per_block = 32 * 1024;
+    const bool no_top = std::getenv("CRT_NO_LDS_TOP") != nullptr;
     if (stack_bytes <= kLdsStackBudget && std::getenv("CRT_FORCE_GSTACK") == nullptr) {
-        W.lds_stack = 0;
-        return launch_render<SE, false, false>(s, device, cam, W, stack_bytes, d_rgb, st, count_stats);
+        const size_t room = per_block > stack_bytes ? per_block - stack_bytes : 0;
+        W.ntop = no_top ? 0 : static_cast<uint32_t>(std::min(s->dnodes.size(), room / sizeof(DevNode)));
+        W.lds_nodes = 0;
+        W.lds_stack = static_cast<uint32_t>(align16(W.ntop * sizeof(DevNode)));
+        return launch_render<SE, false, false>(s, device, cam, W, W.lds_stack + stack_bytes, d_rgb, st, count_stats);
     }
-    return launch_render<SE, true, false>(s, device, cam, W, 0, d_rgb, st, count_stats);
+    W.ntop = no_top ? 0 : static_cast<uint32_t>(std::min(s->dnodes.size(), per_block / sizeof(DevNode)));
+    W.lds_nodes = 0;
+    return launch_render<SE, true, false>(s, device, cam, W, W.ntop * sizeof(DevNode), d_rgb, st, count_stats);
 }
 
 int device_render(const crt_scene* s, int device, const crt_camera* cam, const crt_tiling* t,

@@ -432,11 +432,27 @@ void ppm_pixel_host(const double rgb[3], int32_t out[3]) {
 
 // device-layout staging arrays
 static void stage(crt_scene* s) {
-    s->dnodes.resize(s->nodes.size());
+    // device node array in breadth-first order (the top levels first, so any prefix of it is
+    // a top treelet the render kernel can keep in LDS), children explicit: an interior node's
+    // left child in `flags`, its right child in `index`; a leaf keeps its primitive range and
+    // flags. The traversal visits the same nodes in the same order as over the preorder array.
+    const size_t nn = s->nodes.size();
+    std::vector<uint32_t> bfs, pos(nn, 0);
+    bfs.reserve(nn);
+    if (nn) bfs.push_back(0);
+    for (size_t q = 0; q < bfs.size(); ++q) {
+        const uint32_t i = bfs[q];
+        pos[i] = static_cast<uint32_t>(q);
+        if (s->nodes[i].count == 0 && !(s->nodes[i].flags & kNodeAlways) && i + 1 < nn) {
+            bfs.push_back(i + 1);                  // preorder: the left child follows its parent
+            bfs.push_back(s->nodes[i].index);      // the right child
+        }
+    }
+    s->dnodes.resize(nn);
     s->exact_slab = false;
-    for (size_t i = 0; i < s->nodes.size(); ++i) {
-        const crt_bvh_node& n = s->nodes[i];
-        DevNode& d = s->dnodes[i];
+    for (size_t q = 0; q < bfs.size(); ++q) {
+        const crt_bvh_node& n = s->nodes[bfs[q]];
+        DevNode& d = s->dnodes[q];
         for (int k = 0; k < 3; ++k)
             if (!(n.bounds[2 * k] <= n.bounds[2 * k + 1]) && !(n.flags & kNodeAlways)) s->exact_slab = true;
         std::memcpy(d.b, n.bounds, sizeof d.b);
@@ -445,10 +461,11 @@ static void stage(crt_scene* s) {
                 d.b[2 * k] = -std::numeric_limits<double>::infinity();
                 d.b[2 * k + 1] = std::numeric_limits<double>::infinity();
             }
-        d.index = n.index;
+        const bool inner = n.count == 0 && !(n.flags & kNodeAlways) && bfs[q] + 1 < nn;
+        d.index = inner ? pos[n.index] : n.index;
         d.count = n.count;
         d.axis = n.axis;
-        d.flags = n.flags;
+        d.flags = inner ? pos[bfs[q] + 1] : n.flags;
     }
     // slot arrays: per chunk of slots count the spheres, then fill at prefix offsets (the sphere /
     // parallelogram arrays are in slot order either way)

@@ -18,11 +18,12 @@ constexpr int kMaxDevices = 16;
 // BVH node: the LinearBVHNode of bvh.h:117-161 packed into one 64-byte line (4 x dwordx4 loads).
 struct alignas(16) DevNode {
     double b[6];        // x.min x.max y.min y.max z.min z.max
-    uint32_t index;     // first primitive slot (leaf) / second child (interior)
+    uint32_t index;     // first primitive slot (leaf) / right child (interior)
     uint32_t count;     // primitives in the leaf, 0 for interior
     uint32_t axis;      // split axis (interior)
-    uint32_t flags;     // kNodeAlways: skip the AABB test (linear leaf)
+    uint32_t flags;     // leaf: kNodeAlways = skip the AABB test (linear leaf); interior: left child
 };
+// The device copy lists the nodes breadth-first (crt_host.cpp stage()), children explicit.
 static_assert(sizeof(DevNode) == 64, "node must be one 64-byte line");
 constexpr uint32_t kNodeAlways = 1u;
 
