@@ -73,6 +73,7 @@ struct Work {
     uint32_t sphere_only;   // every primitive is a sphere: refs[slot] == slot
     uint32_t exact_slab;    // the scene needs walk_step's EXACT variant for every ray
     uint32_t ntop;          // HBM-scene kernels: nodes [0, ntop) staged in LDS at lds_nodes
+    uint32_t sentinel;      // the sentinel node's reference (LDS byte offset for LSCENE kernels)
 };
 
 struct Counters {
@@ -418,7 +419,9 @@ struct Trav {
     double inv[3];
     double a;        // dot(d, d)
     double tmax;
-    uint32_t cur, sp, ref;
+    uint32_t cur, ref;
+    int32_t sp;      // stack levels in use; -1 after the pop that follows the last leaf
+    uint32_t first, count;  // the entered leaf's primitive range (walk -> leaf_step)
     uint32_t neg;    // bit k: d[k] < 0; kZeroDir: a slab value may be NaN (walk_step EXACT)
     uint32_t state;
     bool found;
@@ -464,22 +467,49 @@ __device__ __forceinline__ const DevNode* node_at(const SceneView& S, uint32_t i
     return S.nodes + i;
 }
 
-template <typename SE, bool COUNT, bool EXACT, bool TOP>
+// A node reference of the render kernel: LS (LDS-staged scene) kernels address nodes by their
+// LDS byte offset (the staged copy holds interior children as byte offsets, stage_nodes_lds), so
+// a node load needs no address arithmetic; the other kernels use node_at.
+template <bool TOP, bool LS>
+__device__ __forceinline__ const DevNode* node_ref(const SceneView& S, uint32_t cur) {
+    if (LS) return reinterpret_cast<const DevNode*>(reinterpret_cast<const unsigned char*>(S.nodes) + cur);
+    return node_at<TOP>(S, cur);
+}
+
+template <typename SE, bool COUNT, bool EXACT, bool TOP, bool LS, bool GS>
 __device__ __forceinline__ void walk(const SceneView& S, Stack<SE>& st, const double o[3],
                                      double tmin, Trav& R, LaneCounters& ctr) {
-    uint32_t cur = R.cur, sp = R.sp;
-    while (true) {
-        const DevNode* np = node_at<TOP>(S, cur);
-        const uint4 meta = reinterpret_cast<const uint4*>(np)[3];  // index count axis flags
-        const uint32_t top = st.get(sp > 0 ? static_cast<int>(sp) - 1 : 0);  // speculative pop
+    // Every step ends with the next node in `cur`: the near child of an entered interior node,
+    // else the stack top, popped. The level below the stack holds the sentinel node, entered by
+    // every ray, so popping an empty stack leads to the sentinel and the only exit is "entered a
+    // node with primitives" (a leaf, or the sentinel: traversal over). An entered leaf ends the
+    // walk already popped (the reference pops right after the leaf's primitive loop, which leaves
+    // the stack unchanged); its primitive range goes to leaf_step in R.first / R.count. So the
+    // loop body has no branch but that exit, and every lane makes the same updates.
+    // The stack is walked with a pointer to its top level (level sp - 1). The far child is stored
+    // at level sp whatever the outcome (above the live stack unless it is pushed; the stack has
+    // depth + 1 levels); at the sentinel that store rewrites the guard level with the sentinel's
+    // own reference, and the speculative read of the top reads the level below the guard (in
+    // bounds: the host keeps it inside the allocation).
+    const ptrdiff_t stride = static_cast<ptrdiff_t>(st.stride);
+    SE* const empty = st.base - stride;
+    SE* tp = st.base + (static_cast<ptrdiff_t>(R.sp) - 1) * stride;
+    uint32_t cur = R.cur;
+    uint4 meta;
+    bool stop;
+    do {
+        const DevNode* np = node_ref<TOP, LS>(S, cur);
+        meta = reinterpret_cast<const uint4*>(np)[3];  // index count axis flags
+        const uint32_t top = *tp;                         // speculative pop
         if (COUNT) {
-            ctr.nodes++;
+            if (meta.y != kSentinelCount) ctr.nodes++;
             if (wave_leader()) ctr.it_walk++;
         }
         bool enter;
         if (!EXACT) {
-            // linear-mode nodes (kNodeAlways) carry [-inf, inf] bounds in the device copy: with
-            // finite o and finite non-zero inv every slab is (-inf, inf), so they are entered
+            // linear-mode nodes (kNodeAlways) and the sentinel carry [-inf, inf] bounds in the
+            // device copy: with finite o and finite non-zero inv every slab is (-inf, inf), so
+            // they are entered
             const double2* b = reinterpret_cast<const double2*>(np);
             const double2 bx = b[0], by = b[1], bz = b[2];
             const double x0 = (bx.x - o[0]) * R.inv[0], x1 = (bx.y - o[0]) * R.inv[0];
@@ -506,39 +536,41 @@ __device__ __forceinline__ void walk(const SceneView& S, Stack<SE>& st, const do
             const bool c2 = !(xtmin > ztmax || ztmin > xtmax);
             if (ztmin > xtmin) xtmin = ztmin;
             if (ztmax < xtmax) xtmax = ztmax;
-            enter = (c1 & c2 & (xtmin < R.tmax) & (xtmax > tmin)) | (meta.y != 0 && (meta.w & kNodeAlways) != 0);
+            enter = (c1 & c2 & (xtmin < R.tmax) & (xtmax > tmin)) |
+                    (meta.y != 0 && (meta.w & kNodeAlways) != 0) | (meta.y == kSentinelCount);
         }
-        // inner: descend to the near child, push the far one; missed: pop. The far child is
-        // stored at level sp whatever the outcome (level sp is above the live stack unless it is
-        // pushed; the stack has depth + 1 levels), so only the loop exit is a branch: on an
-        // entered leaf (cur stays on it; leaf_step reads its primitive range) or an empty stack.
-        const bool inner = enter && meta.y == 0;
+        const bool inner = enter & (meta.y == 0);
         const bool far_first = (R.neg >> meta.z) & 1u;
         const uint32_t near_child = far_first ? meta.x : meta.w;  // children: left = flags, right = index
         const uint32_t far_child = far_first ? meta.w : meta.x;
-        st.put(static_cast<int>(sp), far_child);
-        if (!inner && (enter || sp == 0)) {
-            R.state = enter ? kLeaf : kDone;
-            break;
-        }
+        tp[stride] = static_cast<SE>(far_child);
+        stop = enter & (meta.y != 0);
         cur = inner ? near_child : top;
-        sp = inner ? sp + 1 : sp - 1;
+        tp += inner ? stride : -stride;
         // once at most kWalkTail lanes still walk, they pause (state stays WALK) and the wave
         // moves on to the leaf phase; they resume in the next round
-        if (kWalkTail > 0 && __popcll(__ballot(1)) <= kWalkTail) break;
-    }
+        if (kWalkTail > 0 && !stop && __popcll(__ballot(1)) <= kWalkTail) {
+            R.cur = cur;
+            R.sp = static_cast<int32_t>(static_cast<uint32_t>(tp - empty) / st.stride);
+            return;
+        }
+    } while (!stop);
+    R.state = meta.y == kSentinelCount ? kDone : kLeaf;
+    R.first = meta.x;
+    R.count = meta.y;
     R.cur = cur;
-    R.sp = sp;
+    // levels in use after the pop; -1 when the leaf was entered with an empty stack
+    R.sp = static_cast<int32_t>(static_cast<uint32_t>(tp - empty)) / static_cast<int32_t>(st.stride);
 }
 
 // the entered leaf's primitives in order (bvh.h:635-652), then "return" to the DFS.
 // Sphere-only scenes store spheres in slot order, so the slot indexes them directly and the next
 // sphere is loaded while the current one is tested.
-template <typename SE, bool COUNT, bool TOP>
+template <typename SE, bool COUNT, bool TOP, bool LS>
 __device__ __forceinline__ void leaf_step(const SceneView& S, Stack<SE>& st, const double o[3],
                                           const double d[3], double tmin, bool sphere_only,
                                           Trav& R, LaneCounters& ctr) {
-    const uint2 range = reinterpret_cast<const uint2*>(node_at<TOP>(S, R.cur))[6];  // index, count
+    const uint2 range = make_uint2(R.first, R.count);  // index, count
     const uint32_t end = range.x + range.y;
     const double ia = recip_a(R.a), lo = lim_tmin(tmin, R.a);
     double hi = lim_tmax(R.tmax, R.a);
@@ -610,12 +642,8 @@ __device__ __forceinline__ void leaf_step(const SceneView& S, Stack<SE>& st, con
             }
         }
     }
-    if (R.sp == 0) {
-        R.state = kDone;
-    } else {
-        R.cur = st.get(--R.sp);
-        R.state = kWalk;
-    }
+    // the pop after the leaf was made by walk (R.cur is the next node, unless the stack was empty)
+    R.state = R.sp < 0 ? kDone : kWalk;
 }
 
 __device__ __forceinline__ uint32_t owned_row(const Work& w, uint32_t k) {
@@ -760,6 +788,22 @@ __device__ __forceinline__ void stage_lds(unsigned char* dst, const void* src, u
     for (uint32_t i = threadIdx.x; i < bytes / 16; i += kBlock) d[i] = s[i];
 }
 
+// the node array staged at LDS offset 0 with interior children (count == 0: left = flags, right =
+// index) and the sentinel's self references rewritten as byte offsets, the node references of LS
+// kernels (node_ref)
+__device__ __forceinline__ void stage_nodes_lds(unsigned char* dst, const DevNode* src, uint32_t bytes) {
+    const uint4* s = reinterpret_cast<const uint4*>(src);
+    uint4* d = reinterpret_cast<uint4*>(dst);
+    for (uint32_t i = threadIdx.x; i < bytes / 16; i += kBlock) {
+        uint4 v = s[i];
+        if ((i & 3u) == 3u && (v.y == 0 || v.y == kSentinelCount)) {
+            v.x *= static_cast<uint32_t>(sizeof(DevNode));
+            v.w *= static_cast<uint32_t>(sizeof(DevNode));
+        }
+        d[i] = v;
+    }
+}
+
 // The render kernel. Thread -> (sample chunk, pixel); each wave starts on one 8x8 pixel tile.
 // Persistent per-lane state machine (WALK -> LEAF -> ... -> DONE -> shade -> WALK) in traversal
 // rounds: every walking lane walks the DFS to its next entered leaf (or the end of its
@@ -783,12 +827,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRT_WAVE
     Counters* __restrict__ counters) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     SceneView S = Sg;
-    if (LSCENE) {
-        stage_lds(smem + W.lds_nodes, Sg.nodes, W.bytes_nodes);
+    if (LSCENE) {  // nodes at LDS offset 0 (node_ref: a node's LDS address is its byte offset)
+        stage_nodes_lds(smem, Sg.nodes, W.bytes_nodes);
         stage_lds(smem + W.lds_refs, Sg.refs, W.bytes_refs);
         stage_lds(smem + W.lds_spheres, Sg.spheres, W.bytes_spheres);
         stage_lds(smem + W.lds_quads, Sg.quads, W.bytes_quads);
-        S.nodes = reinterpret_cast<const DevNode*>(smem + W.lds_nodes);
+        S.nodes = reinterpret_cast<const DevNode*>(smem);
         S.refs = reinterpret_cast<const uint32_t*>(smem + W.lds_refs);
         S.spheres = reinterpret_cast<const DevSphere*>(smem + W.lds_spheres);
         S.quads = reinterpret_cast<const DevQuad*>(smem + W.lds_quads);
@@ -811,14 +855,18 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRT_WAVE
     const uint32_t col = tx * 8 + (lane & 7);
     const uint32_t k = ty * 8 + (lane >> 3);
     const bool valid = chunk < W.chunks && col < C.w && k < W.owned_rows;
+    // stack levels 0..depth of this lane, above a guard level holding the sentinel reference
+    // and one more level walk() may read (two guard levels in HBM; in LDS the level below the
+    // guard is other data)
     Stack<SE> st;
     if (GSTACK) {
-        st.base = gstack + (static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x);
         st.stride = gridDim.x * kBlock;
+        st.base = gstack + (static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x) + 2 * static_cast<size_t>(st.stride);
     } else {
         st.base = reinterpret_cast<SE*>(smem + W.lds_stack) + threadIdx.x;
         st.stride = kBlock;
     }
+    st.base[-static_cast<ptrdiff_t>(st.stride)] = static_cast<SE>(W.sentinel);
     const uint32_t row = valid ? owned_row(W, k) : 0;
     const uint32_t pixel = row * C.w + col;
     uint32_t s = chunk * W.chunk_len;
@@ -841,13 +889,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRT_WAVE
         while (true) {
             if (COUNT) cw -= static_cast<uint32_t>(wall_clock64());
             if (!W.exact_slab && __ballot(R.state == kWalk && (R.neg & kZeroDir)) == 0) {
-                if (R.state == kWalk) walk<SE, COUNT, false, !LSCENE>(S, st, P.o, C.t_min, R, ctr);
+                if (R.state == kWalk) walk<SE, COUNT, false, !LSCENE, LSCENE, GSTACK>(S, st, P.o, C.t_min, R, ctr);
             } else {
-                if (R.state == kWalk) walk<SE, COUNT, true, !LSCENE>(S, st, P.o, C.t_min, R, ctr);
+                if (R.state == kWalk) walk<SE, COUNT, true, !LSCENE, LSCENE, GSTACK>(S, st, P.o, C.t_min, R, ctr);
             }
             if (COUNT) cw += static_cast<uint32_t>(wall_clock64());
             if (COUNT) cl -= static_cast<uint32_t>(wall_clock64());
-            if (R.state == kLeaf) leaf_step<SE, COUNT, !LSCENE>(S, st, P.o, P.d, C.t_min, W.sphere_only != 0, R, ctr);
+            if (R.state == kLeaf) leaf_step<SE, COUNT, !LSCENE, LSCENE>(S, st, P.o, P.d, C.t_min, W.sphere_only != 0, R, ctr);
             if (COUNT) cl += static_cast<uint32_t>(wall_clock64());
             const uint64_t pending = __ballot(R.state == kWalk);
             const uint64_t finished = __ballot(R.state == kDone);
@@ -1157,7 +1205,7 @@ static int launch_render(const crt_scene* s, int device, const crt_camera* cam, 
     if (!count)
         HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&partial), plane * W.chunks * sizeof(double), stream));
     if (GSTACK) {
-        size_t bytes = static_cast<size_t>(s->depth + 1) * blocks * dev::kBlock * sizeof(SE);
+        size_t bytes = static_cast<size_t>(s->depth + 3) * blocks * dev::kBlock * sizeof(SE);  // + 2 guard levels
         HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&gstack), bytes, stream));
     }
     if (count) {
@@ -1232,14 +1280,20 @@ static int dispatch_render(const crt_scene* s, int device, const crt_camera* cam
     W.bytes_spheres = static_cast<uint32_t>(align16(s->spheres.size() * sizeof(DevSphere)));
     W.bytes_quads = static_cast<uint32_t>(align16(s->quads.size() * sizeof(DevQuad)));
     const size_t scene_bytes = static_cast<size_t>(W.bytes_nodes) + W.bytes_refs + W.bytes_spheres + W.bytes_quads;
+    const uint32_t level = static_cast<uint32_t>(dev::kBlock * sizeof(SE));  // one stack level
+    const uint32_t nn = static_cast<uint32_t>(s->dnodes.size() - 1);      // the sentinel's index
     const bool force_global = std::getenv("CRT_NO_LDS_SCENE") != nullptr;
-    if (!force_global && scene_bytes + stack_bytes <= kLdsSceneBudget) {
+    // LDS stacks: [data][guard level: sentinel][levels 0..depth]; walk() may also read the level
+    // below the guard, so the guard starts at least one level into the allocation
+    auto stack_at = [&](size_t data_bytes) { return static_cast<uint32_t>(std::max<size_t>(data_bytes, level) + level); };
+    if (!force_global && stack_at(scene_bytes) + stack_bytes <= kLdsSceneBudget) {
         W.lds_nodes = 0;
         W.lds_refs = W.lds_nodes + W.bytes_nodes;
         W.lds_spheres = W.lds_refs + W.bytes_refs;
         W.lds_quads = W.lds_spheres + W.bytes_spheres;
-        W.lds_stack = W.lds_quads + W.bytes_quads;
-        return launch_render<SE, false, true>(s, device, cam, W, scene_bytes + stack_bytes, d_rgb, st, count_stats);
+        W.lds_stack = stack_at(scene_bytes);
+        W.sentinel = nn * static_cast<uint32_t>(sizeof(DevNode));  // LDS byte offset
+        return launch_render<SE, false, true>(s, device, cam, W, W.lds_stack + stack_bytes, d_rgb, st, count_stats);
     }
     // HBM scene: the top of the (breadth-first) node array goes to LDS as far as it fits beside
     // the stack without costing resident blocks (5 blocks of 4 waves, the VGPR limit, at
@@ -1247,14 +1301,16 @@ static int dispatch_render(const crt_scene* s, int device, const crt_camera* cam
     const size_t per_block = 32 * 1024;
     const bool no_top = std::getenv("CRT_NO_LDS_TOP") != nullptr;
     if (stack_bytes <= kLdsStackBudget && std::getenv("CRT_FORCE_GSTACK") == nullptr) {
-        const size_t room = per_block > stack_bytes ? per_block - stack_bytes : 0;
+        const size_t room = per_block > stack_bytes + 2 * level ? per_block - stack_bytes - 2 * level : 0;
         W.ntop = no_top ? 0 : static_cast<uint32_t>(std::min(s->dnodes.size(), room / sizeof(DevNode)));
         W.lds_nodes = 0;
-        W.lds_stack = static_cast<uint32_t>(align16(W.ntop * sizeof(DevNode)));
+        W.lds_stack = stack_at(align16(W.ntop * sizeof(DevNode)));
+        W.sentinel = nn;
         return launch_render<SE, false, false>(s, device, cam, W, W.lds_stack + stack_bytes, d_rgb, st, count_stats);
     }
     W.ntop = no_top ? 0 : static_cast<uint32_t>(std::min(s->dnodes.size(), per_block / sizeof(DevNode)));
     W.lds_nodes = 0;
+    W.sentinel = nn;
     return launch_render<SE, true, false>(s, device, cam, W, W.ntop * sizeof(DevNode), d_rgb, st, count_stats);
 }
 

@@ -448,8 +448,18 @@ static void stage(crt_scene* s) {
             bfs.push_back(s->nodes[i].index);      // the right child
         }
     }
-    s->dnodes.resize(nn);
+    s->dnodes.resize(nn + 1);
     s->exact_slab = false;
+    {  // the sentinel (kSentinelCount) after the tree's nodes
+        DevNode& z = s->dnodes[nn];
+        for (int k = 0; k < 3; ++k) {
+            z.b[2 * k] = -std::numeric_limits<double>::infinity();
+            z.b[2 * k + 1] = std::numeric_limits<double>::infinity();
+        }
+        z.index = z.flags = static_cast<uint32_t>(nn);
+        z.count = kSentinelCount;
+        z.axis = 0;
+    }
     for (size_t q = 0; q < bfs.size(); ++q) {
         const crt_bvh_node& n = s->nodes[bfs[q]];
         DevNode& d = s->dnodes[q];

@@ -26,6 +26,11 @@ struct alignas(16) DevNode {
 // The device copy lists the nodes breadth-first (crt_host.cpp stage()), children explicit.
 static_assert(sizeof(DevNode) == 64, "node must be one 64-byte line");
 constexpr uint32_t kNodeAlways = 1u;
+// The device node array ends with a sentinel node (index = node count): box [-inf, inf]^3, count
+// kSentinelCount, both children itself. The render kernel keeps a reference to it in a guard
+// level below each lane's stack, so popping an empty stack lands on the sentinel, and the walk
+// loop's only exit test is "entered a node with a primitive count" (crt_device.hip walk()).
+constexpr uint32_t kSentinelCount = 0xffffffffu;
 
 // Sphere (sphere.h:16-18): centre + radius in one 32-byte record.
 struct alignas(16) DevSphere {
