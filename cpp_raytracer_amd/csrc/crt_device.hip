@@ -253,18 +253,31 @@ __device__ __forceinline__ bool hit_sphere(const DevSphere& sp, const double o[3
     return true;
 }
 
-// hit_sphere's cheap part only: false when the sphere provably cannot be accepted for any
-// t_max' <= the t_max behind `hi` (no real root, or both roots outside (t_min, t_max)).
+// The candidate filter of two-pass sphere leaves: false only when the exact test (hit_sphere,
+// i.e. Sphere::hit_by) provably rejects the sphere for every t_max' <= the t_max behind `hi`.
+// No square root: with y = -b - hi and w = b + lo,
+//   no real root          <=  D < 0
+//   both roots >= t_max   <=  y > 0 and y^2 > D
+//   both roots <= t_min   <=  w > 0 and w^2 > D
+// where D = disc' + 2^-30 S + 2^-500 bounds the exact test's disc from above: disc' is evaluated
+// with fused multiply-adds, and |disc' - disc| <= 31 u S with S = a (|oc|^2 + r^2) >= |disc| / 2,
+// u = 2^-53 (each of b, |oc|^2, c is within 5u of its exact value in both evaluations). The
+// 2^-30 S slack also covers the error of b' in y and w; lo / hi (lim_tmin / lim_tmax) carry the
+// 2^-30 relative slack for the rounding of the exact roots. NaN or inf anywhere rejects nothing.
+// Valid for a = dot(d, d) in [2^-500, 2^500] (leaf_step checks). tools/fuzz_sphere_filter.c
+// checks it against the exact test on tangent, self-intersecting and wide-range cases.
 __device__ __forceinline__ bool sphere_candidate(const DevSphere& sp, const double o[3], const double d[3],
                                                  double a, double lo, double hi) {
-    double ocx = o[0] - sp.c[0], ocy = o[1] - sp.c[1], ocz = o[2] - sp.c[2];
-    double b = d[0] * ocx + d[1] * ocy + d[2] * ocz;
-    double c = (ocx * ocx + ocy * ocy + ocz * ocz) - sp.r * sp.r;
-    double disc = b * b - a * c;
-    if (disc < 0) return false;
-    const double sqa = disc * __builtin_amdgcn_rsq(disc);
-    const double m = (fabs(b) + sqa) * 0x1p-12;
-    return !((-b - sqa) - m > hi || (-b + sqa) + m < lo);
+    const double ocx = o[0] - sp.c[0], ocy = o[1] - sp.c[1], ocz = o[2] - sp.c[2];
+    const double b = fma(d[2], ocz, fma(d[1], ocy, d[0] * ocx));
+    const double q = fma(ocz, ocz, fma(ocy, ocy, ocx * ocx));
+    const double r2 = sp.r * sp.r;
+    const double disc = fma(b, b, -(a * (q - r2)));
+    const double D = fma(a * (q + r2), 0x1p-30, disc) + 0x1p-500;
+    const double y = -b - hi, w = b + lo;
+    // for D >= 0, "y > 0 and y^2 > D" is y |y| > D
+    const bool rej = (D < 0) | (y * fabs(y) > D) | (w * fabs(w) > D);
+    return !rej;
 }
 
 // Parallelogram::hit_by (parallelogram.h:177-240)
@@ -574,26 +587,33 @@ __device__ __forceinline__ void leaf_step(const SceneView& S, Stack<SE>& st, con
     const uint32_t end = range.x + range.y;
     const double ia = recip_a(R.a), lo = lim_tmin(tmin, R.a);
     double hi = lim_tmax(R.tmax, R.a);
-    if (sphere_only && range.y <= 32) {
+    if (sphere_only && range.y <= 32 && R.a >= 0x1p-500 && R.a <= 0x1p500) {
         // two passes: the cheap candidate test of every sphere against the leaf-entry t_max, then
         // the full test of the candidates in slot order with the shrinking t_max. A sphere the
         // first pass rejects is rejected by the full test for any smaller t_max too, so the hits
         // and the tie order are the sequential loop's; the full-test pass runs only as often as
         // the lane with most candidates needs (typically 1-3 of 6-12).
+        // Pass 1 runs over pairs (the loads of one half overlap the tests of the other, with no
+        // register rotation) and shifts each verdict into `cand`: after the pass, bit
+        // nbits - 1 - i stands for sphere i (nbits = count rounded up to even; the odd count's
+        // extra test reads the slot after the leaf, inside the scene copy, and is masked off).
         uint32_t cand = 0;
-        DevSphere cur = S.spheres[range.x];
-        for (uint32_t i = 0; i < range.y; ++i) {
-            const DevSphere nxt = S.spheres[range.x + i + 1];
+        const uint32_t nbits = (range.y + 1) & ~1u;
+        DevSphere s0 = S.spheres[range.x];
+        for (uint32_t i = 0; i < range.y; i += 2) {
+            const DevSphere s1 = S.spheres[range.x + i + 1];
             if (COUNT) {
-                ctr.sphere_tests++;
-                if (wave_leader()) ctr.it_leaf++;
+                ctr.sphere_tests += i + 1 < range.y ? 2 : 1;
+                if (wave_leader()) ctr.it_leaf += 2;
             }
-            if (sphere_candidate(cur, o, d, R.a, lo, hi)) cand |= 1u << i;
-            cur = nxt;
+            cand = (cand << 1) | static_cast<uint32_t>(sphere_candidate(s0, o, d, R.a, lo, hi));
+            s0 = S.spheres[range.x + i + 2];
+            cand = (cand << 1) | static_cast<uint32_t>(sphere_candidate(s1, o, d, R.a, lo, hi) & (i + 1 < range.y));
         }
         while (cand) {
-            const uint32_t i = range.x + __builtin_ctz(cand);
-            cand &= cand - 1;
+            const uint32_t b = 31 - __builtin_clz(cand);
+            cand ^= 1u << b;
+            const uint32_t i = range.x + (nbits - 1 - b);
             double t;
             if (hit_sphere(S.spheres[i], o, d, R.a, ia, tmin, R.tmax, lo, hi, t)) {
                 R.tmax = t;
