@@ -276,8 +276,8 @@ __device__ __forceinline__ bool sphere_candidate(const DevSphere& sp, const doub
     const double D = fma(a * (q + r2), 0x1p-30, disc) + 0x1p-500;
     const double y = -b - hi, w = b + lo;
     // for D >= 0, "y > 0 and y^2 > D" is y |y| > D
-    const bool rej = (D < 0) | (y * fabs(y) > D) | (w * fabs(w) > D);
-    return !rej;
+    const int rej = static_cast<int>(D < 0) | static_cast<int>(y * fabs(y) > D) | static_cast<int>(w * fabs(w) > D);
+    return rej == 0;
 }
 
 // Parallelogram::hit_by (parallelogram.h:177-240)
@@ -483,9 +483,12 @@ __device__ __forceinline__ const DevNode* node_at(const SceneView& S, uint32_t i
 // A node reference of the render kernel: LS (LDS-staged scene) kernels address nodes by their
 // LDS byte offset (the staged copy holds interior children as byte offsets, stage_nodes_lds), so
 // a node load needs no address arithmetic; the other kernels use node_at.
+// (The LDS pointer is made from the offset itself: the kernel's dynamic LDS starts at LDS
+// address 0, which render_kernel checks, so no base address is added per node.)
+typedef __attribute__((address_space(3))) const unsigned char LdsByte;
 template <bool TOP, bool LS>
 __device__ __forceinline__ const DevNode* node_ref(const SceneView& S, uint32_t cur) {
-    if (LS) return reinterpret_cast<const DevNode*>(reinterpret_cast<const unsigned char*>(S.nodes) + cur);
+    if (LS) return (const DevNode*)(LdsByte*)static_cast<uintptr_t>(cur);
     return node_at<TOP>(S, cur);
 }
 
@@ -557,7 +560,7 @@ __device__ __forceinline__ void walk(const SceneView& S, Stack<SE>& st, const do
         const uint32_t near_child = far_first ? meta.x : meta.w;  // children: left = flags, right = index
         const uint32_t far_child = far_first ? meta.w : meta.x;
         tp[stride] = static_cast<SE>(far_child);
-        stop = enter & (meta.y != 0);
+        stop = enter ^ inner;  // entered, not interior: a leaf or the sentinel
         cur = inner ? near_child : top;
         tp += inner ? stride : -stride;
         // once at most kWalkTail lanes still walk, they pause (state stays WALK) and the wave
@@ -848,6 +851,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRT_WAVE
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     SceneView S = Sg;
     if (LSCENE) {  // nodes at LDS offset 0 (node_ref: a node's LDS address is its byte offset)
+        if (static_cast<uint32_t>(reinterpret_cast<uintptr_t>((LdsByte*)smem)) != 0) __builtin_trap();
         stage_nodes_lds(smem, Sg.nodes, W.bytes_nodes);
         stage_lds(smem + W.lds_refs, Sg.refs, W.bytes_refs);
         stage_lds(smem + W.lds_spheres, Sg.spheres, W.bytes_spheres);
