@@ -227,6 +227,8 @@ __device__ __forceinline__ double div_a(double n, double a, double ia) {
 __device__ __forceinline__ double lim_tmax(double tmax, double a) { return tmax * a * (1 + 0x1p-30); }
 __device__ __forceinline__ double lim_tmin(double tmin, double a) { return tmin * a * (1 - 0x1p-30); }
 
+// COARSE = false skips the coarse reject (the candidates of two-pass leaves passed a filter).
+template <bool COARSE = true>
 __device__ __forceinline__ bool hit_sphere(const DevSphere& sp, const double o[3], const double d[3],
                                            double a, double ia, double tmin, double tmax, double lo,
                                            double hi, double& t) {
@@ -236,7 +238,7 @@ __device__ __forceinline__ bool hit_sphere(const DevSphere& sp, const double o[3
     double disc = b * b - a * c;
     if (disc < 0) return false;
     const double rs = __builtin_amdgcn_rsq(disc);
-    {
+    if (COARSE) {
         const double sqa = disc * rs;                              // ~sqrt(disc)
         const double m = (fabs(b) + sqa) * 0x1p-12;                // covers every rounding error
         const bool beyond = (-b - sqa) - m > hi;   // r1 > tmax, so r2 too  (hi = lim_tmax)
@@ -618,7 +620,10 @@ __device__ __forceinline__ void leaf_step(const SceneView& S, Stack<SE>& st, con
             cand ^= 1u << b;
             const uint32_t i = range.x + (nbits - 1 - b);
             double t;
-            if (hit_sphere(S.spheres[i], o, d, R.a, ia, tmin, R.tmax, lo, hi, t)) {
+#ifndef CRT_P2_COARSE
+#define CRT_P2_COARSE 0
+#endif
+            if (hit_sphere<CRT_P2_COARSE != 0>(S.spheres[i], o, d, R.a, ia, tmin, R.tmax, lo, hi, t)) {
                 R.tmax = t;
                 hi = lim_tmax(t, R.a);
                 R.ref = i;
