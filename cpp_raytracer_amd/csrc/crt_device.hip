@@ -74,6 +74,7 @@ struct Work {
     uint32_t exact_slab;    // the scene needs walk_step's EXACT variant for every ray
     uint32_t ntop;          // HBM-scene kernels: nodes [0, ntop) staged in LDS at lds_nodes
     uint32_t sentinel;      // the sentinel node's reference (LDS byte offset for LSCENE kernels)
+    uint32_t lds_cam;       // LDS copy of the CamView (read where used: keeps it out of SGPRs)
 };
 
 struct Counters {
@@ -704,7 +705,11 @@ __device__ __forceinline__ void start_path(const CamView& C, uint32_t row, uint3
         P.o[1] = (C.o[1] + C.ddx[1] * vx) + C.ddy[1] * vy;
         P.o[2] = (C.o[2] + C.ddx[2] * vx) + C.ddy[2] * vy;
     }
-    const double fr = static_cast<double>(row), fc = static_cast<double>(col);
+    // converted here at every call: hoisted out of the kernel's loop, the two doubles would
+    // stay live (and spill) across all phases
+    uint32_t ir = row, ic = col;
+    asm volatile("" : "+v"(ir), "+v"(ic));
+    const double fr = static_cast<double>(ir), fc = static_cast<double>(ic);
     // a g++ build evaluates the second jitter draw (the pixel_delta_y one) first
     const double uy = rnd(rng, -0.5, 0.5);
     const double ux = rnd(rng, -0.5, 0.5);
@@ -872,6 +877,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRT_WAVE
         S.ntop = W.ntop;
         __syncthreads();
     }
+    // The camera constants are read from an LDS copy in start_path / shade: held in SGPRs for
+    // the whole kernel they would spill (into VGPR lanes, reloaded with v_readlane per use).
+    if (threadIdx.x == 0) *reinterpret_cast<CamView*>(smem + W.lds_cam) = C;
+    __syncthreads();
+    const CamView& CL = *reinterpret_cast<const CamView*>(smem + W.lds_cam);
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t wave = (static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x) >> 6;
     // tile-major: the chunks of one 8x8 tile are consecutive waves, so the four waves of a block
@@ -906,7 +916,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRT_WAVE
     R.state = kIdle;
     // max_depth == 0: ray_color returns RGB::zero() for every sample (camera.h:211-213)
     if (valid && C.max_depth > 0 && s < s_end) {
-        start_path(C, row, col, sample_seed(C.base_seed, pixel, s), P);
+        start_path(CL, row, col, sample_seed(C.base_seed, pixel, s), P);
         trav_init(P.o, P.d, R);
         if (COUNT) ctr.rays++;
     }
@@ -937,12 +947,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRT_WAVE
             if (COUNT) cs -= static_cast<uint32_t>(wall_clock64());
             if (R.state == kDone) {
                 if (COUNT && wave_leader()) ctr.it_shade++;
-                bool ended = shade(S, C, P, R.found, R.ref, R.tmax, acc);
+                bool ended = shade(S, CL, P, R.found, R.ref, R.tmax, acc);
                 // a scattered ray with no bounce left returns RGB::zero() (camera.h:211-213)
                 if (!ended && P.depth == 0) ended = true;
                 if (ended) {
                     if (++s >= s_end) R.state = kIdle;
-                    else start_path(C, row, col, sample_seed(C.base_seed, pixel, s), P);
+                    else start_path(CL, row, col, sample_seed(C.base_seed, pixel, s), P);
                 }
                 if (R.state != kIdle) {
                     trav_init(P.o, P.d, R);
@@ -1210,6 +1220,8 @@ static int launch_render(const crt_scene* s, int device, const crt_camera* cam, 
                          size_t lds, double* d_rgb, hipStream_t stream, crt_render_stats* count_stats) {
     const DeviceCopy& c = s->dev[device];
     dev::Work W = w0;
+    W.lds_cam = static_cast<uint32_t>(align16(lds));  // the camera copy after the rest
+    lds = W.lds_cam + align16(sizeof(dev::CamView));
     const uint64_t pixels = static_cast<uint64_t>(W.owned_rows) * cam->image_w;
     // Sample chunks: a function of spp ONLY, so every pixel's sum is grouped identically whatever
     // the tiling / number of GPUs (bit-identical frames for 1..N devices). 24-sample chunks
