@@ -495,6 +495,35 @@ __device__ __forceinline__ const DevNode* node_ref(const SceneView& S, uint32_t 
     return node_at<TOP>(S, cur);
 }
 
+// The four 16-byte lines of node `cur` (see node_ref). TOP kernels read a top-treelet node from
+// LDS and any other from HBM with separate, masked loads into the same registers (no per-lane
+// pointer select, no flat loads).
+typedef double Dvec2 __attribute__((ext_vector_type(2)));
+typedef uint32_t Uvec4 __attribute__((ext_vector_type(4)));
+struct NodeLines {
+    Dvec2 b[3];  // (x.min, x.max), (y.min, y.max), (z.min, z.max)
+    Uvec4 meta;  // index count axis flags
+};
+template <typename P>
+__device__ __forceinline__ void node_lines(P p, NodeLines& n) {
+    n.b[0] = p->b[0];
+    n.b[1] = p->b[1];
+    n.b[2] = p->b[2];
+    n.meta = p->meta;
+}
+typedef __attribute__((address_space(3))) const NodeLines LdsNode;
+typedef __attribute__((address_space(1))) const NodeLines GlobalNode;
+template <bool TOP, bool LS>
+__device__ __forceinline__ void fetch_node(const SceneView& S, uint32_t cur, NodeLines& n) {
+    if (LS) {
+        node_lines((LdsNode*)static_cast<uintptr_t>(cur), n);
+    } else if (TOP && cur < S.ntop) {  // the treelet sits at LDS offset 0 (render_kernel checks)
+        node_lines((LdsNode*)static_cast<uintptr_t>(cur * static_cast<uint32_t>(sizeof(DevNode))), n);
+    } else {
+        node_lines((GlobalNode*)(S.nodes + cur), n);
+    }
+}
+
 template <typename SE, bool COUNT, bool EXACT, bool TOP, bool LS, bool GS>
 __device__ __forceinline__ void walk(const SceneView& S, Stack<SE>& st, const double o[3],
                                      double tmin, Trav& R, LaneCounters& ctr) {
@@ -517,8 +546,9 @@ __device__ __forceinline__ void walk(const SceneView& S, Stack<SE>& st, const do
     uint4 meta;
     bool stop;
     do {
-        const DevNode* np = node_ref<TOP, LS>(S, cur);
-        meta = reinterpret_cast<const uint4*>(np)[3];  // index count axis flags
+        NodeLines nd;
+        fetch_node<TOP, LS>(S, cur, nd);
+        meta = make_uint4(nd.meta.x, nd.meta.y, nd.meta.z, nd.meta.w);  // index count axis flags
         const uint32_t top = *tp;                         // speculative pop
         if (COUNT) {
             if (meta.y != kSentinelCount) ctr.nodes++;
@@ -529,8 +559,7 @@ __device__ __forceinline__ void walk(const SceneView& S, Stack<SE>& st, const do
             // linear-mode nodes (kNodeAlways) and the sentinel carry [-inf, inf] bounds in the
             // device copy: with finite o and finite non-zero inv every slab is (-inf, inf), so
             // they are entered
-            const double2* b = reinterpret_cast<const double2*>(np);
-            const double2 bx = b[0], by = b[1], bz = b[2];
+            const Dvec2 bx = nd.b[0], by = nd.b[1], bz = nd.b[2];
             const double x0 = (bx.x - o[0]) * R.inv[0], x1 = (bx.y - o[0]) * R.inv[0];
             const double y0 = (by.x - o[1]) * R.inv[1], y1 = (by.y - o[1]) * R.inv[1];
             const double z0 = (bz.x - o[2]) * R.inv[2], z1 = (bz.y - o[2]) * R.inv[2];
@@ -538,11 +567,11 @@ __device__ __forceinline__ void walk(const SceneView& S, Stack<SE>& st, const do
             const double far = fmin(fmin(fmax(x0, x1), fmax(y0, y1)), fmax(z0, z1));
             enter = (near <= far) & (near < R.tmax) & (far > tmin);
         } else {
-            const double* b = reinterpret_cast<const double*>(np);
-            const uint32_t nx = R.neg & 1u, ny = (R.neg >> 1) & 1u, nz = (R.neg >> 2) & 1u;
-            const double bx0 = b[0 + nx], bx1 = b[1 - nx];
-            const double by0 = b[2 + ny], by1 = b[3 - ny];
-            const double bz0 = b[4 + nz], bz1 = b[5 - nz];
+            // x[neg] / x[!neg]
+            const bool nx = R.neg & 1u, ny = (R.neg >> 1) & 1u, nz = (R.neg >> 2) & 1u;
+            const double bx0 = nx ? nd.b[0].y : nd.b[0].x, bx1 = nx ? nd.b[0].x : nd.b[0].y;
+            const double by0 = ny ? nd.b[1].y : nd.b[1].x, by1 = ny ? nd.b[1].x : nd.b[1].y;
+            const double bz0 = nz ? nd.b[2].y : nd.b[2].x, bz1 = nz ? nd.b[2].x : nd.b[2].y;
             double xtmin = (bx0 - o[0]) * R.inv[0];
             double xtmax = (bx1 - o[0]) * R.inv[0];
             const double ytmin = (by0 - o[1]) * R.inv[1];
@@ -854,6 +883,11 @@ __device__ __forceinline__ void stage_nodes_lds(unsigned char* dst, const DevNod
 #endif
 constexpr int kShadeBatch = CRT_SHADE_BATCH;
 
+#ifndef CRT_TOP_TREELET
+#define CRT_TOP_TREELET 1
+#endif
+constexpr bool kTopTreelet = CRT_TOP_TREELET != 0;
+
 template <typename SE, bool GSTACK, bool LSCENE, bool COUNT>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRT_WAVES_PER_EU, 8))) void render_kernel(
     SceneView Sg, CamView C, Work W, double* __restrict__ partial, SE* __restrict__ gstack,
@@ -872,6 +906,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRT_WAVE
         S.quads = reinterpret_cast<const DevQuad*>(smem + W.lds_quads);
         __syncthreads();
     } else if (W.ntop) {  // HBM scene: keep its top ntop nodes (breadth-first) in LDS
+        if (static_cast<uint32_t>(reinterpret_cast<uintptr_t>((LdsByte*)smem)) != 0) __builtin_trap();
         stage_lds(smem + W.lds_nodes, Sg.nodes, W.ntop * static_cast<uint32_t>(sizeof(DevNode)));
         S.top_nodes = reinterpret_cast<const DevNode*>(smem + W.lds_nodes);
         S.ntop = W.ntop;
@@ -928,13 +963,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRT_WAVE
         while (true) {
             if (COUNT) cw -= static_cast<uint32_t>(wall_clock64());
             if (!W.exact_slab && __ballot(R.state == kWalk && (R.neg & kZeroDir)) == 0) {
-                if (R.state == kWalk) walk<SE, COUNT, false, !LSCENE, LSCENE, GSTACK>(S, st, P.o, C.t_min, R, ctr);
+                if (R.state == kWalk) walk<SE, COUNT, false, kTopTreelet && !LSCENE, LSCENE, GSTACK>(S, st, P.o, C.t_min, R, ctr);
             } else {
-                if (R.state == kWalk) walk<SE, COUNT, true, !LSCENE, LSCENE, GSTACK>(S, st, P.o, C.t_min, R, ctr);
+                if (R.state == kWalk) walk<SE, COUNT, true, kTopTreelet && !LSCENE, LSCENE, GSTACK>(S, st, P.o, C.t_min, R, ctr);
             }
             if (COUNT) cw += static_cast<uint32_t>(wall_clock64());
             if (COUNT) cl -= static_cast<uint32_t>(wall_clock64());
-            if (R.state == kLeaf) leaf_step<SE, COUNT, !LSCENE, LSCENE>(S, st, P.o, P.d, C.t_min, W.sphere_only != 0, R, ctr);
+            if (R.state == kLeaf) leaf_step<SE, COUNT, kTopTreelet && !LSCENE, LSCENE>(S, st, P.o, P.d, C.t_min, W.sphere_only != 0, R, ctr);
             if (COUNT) cl += static_cast<uint32_t>(wall_clock64());
             const uint64_t pending = __ballot(R.state == kWalk);
             const uint64_t finished = __ballot(R.state == kDone);

@@ -432,22 +432,45 @@ void ppm_pixel_host(const double rgb[3], int32_t out[3]) {
 
 // device-layout staging arrays
 static void stage(crt_scene* s) {
-    // device node array in breadth-first order (the top levels first, so any prefix of it is
-    // a top treelet the render kernel can keep in LDS), children explicit: an interior node's
-    // left child in `flags`, its right child in `index`; a leaf keeps its primitive range and
-    // flags. The traversal visits the same nodes in the same order as over the preorder array.
+    // Device node array, children explicit: an interior node's left child in `flags`, its right
+    // child in `index`; a leaf keeps its primitive range and flags. The traversal visits the same
+    // nodes in the same order as over the preorder array. Order: breadth-first for the first
+    // kTopBfs nodes (the top levels, so any prefix of them is a top treelet the render kernel can
+    // keep in LDS), then each remaining subtree depth-first with siblings side by side (a node's
+    // two children share a 128-byte line, and a subtree is contiguous: cache locality for trees
+    // that live in HBM).
+    constexpr size_t kTopBfs = 1024;
     const size_t nn = s->nodes.size();
+    auto interior = [&](uint32_t i) {
+        return s->nodes[i].count == 0 && !(s->nodes[i].flags & kNodeAlways) && i + 1 < nn;
+    };
     std::vector<uint32_t> bfs, pos(nn, 0);
     bfs.reserve(nn);
     if (nn) bfs.push_back(0);
-    for (size_t q = 0; q < bfs.size(); ++q) {
+    size_t q = 0;
+    for (; q < bfs.size() && bfs.size() < kTopBfs; ++q) {
         const uint32_t i = bfs[q];
-        pos[i] = static_cast<uint32_t>(q);
-        if (s->nodes[i].count == 0 && !(s->nodes[i].flags & kNodeAlways) && i + 1 < nn) {
+        if (interior(i)) {
             bfs.push_back(i + 1);                  // preorder: the left child follows its parent
             bfs.push_back(s->nodes[i].index);      // the right child
         }
     }
+    {  // placed but not yet expanded: bfs[q, size0); expand each subtree in sibling-pair DFS
+        const size_t size0 = bfs.size();
+        std::vector<uint32_t> todo;
+        for (size_t r = size0; r-- > q;) todo.push_back(bfs[r]);  // so bfs[q] is expanded first
+        while (!todo.empty()) {
+            const uint32_t i = todo.back();
+            todo.pop_back();
+            if (!interior(i)) continue;
+            const uint32_t l = i + 1, rr = s->nodes[i].index;
+            bfs.push_back(l);
+            bfs.push_back(rr);
+            todo.push_back(rr);
+            todo.push_back(l);
+        }
+    }
+    for (size_t k = 0; k < bfs.size(); ++k) pos[bfs[k]] = static_cast<uint32_t>(k);
     s->dnodes.resize(nn + 1);
     s->exact_slab = false;
     {  // the sentinel (kSentinelCount) after the tree's nodes
