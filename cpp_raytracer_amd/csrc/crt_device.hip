@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <limits>
@@ -34,19 +35,20 @@ namespace dev {
 #ifndef CRT_BLOCK
 #define CRT_BLOCK 256
 #endif
-#ifndef CRT_WALK_TAIL
-#define CRT_WALK_TAIL 0
-#endif
 constexpr int kBlock = CRT_BLOCK;
-constexpr int kWalkTail = CRT_WALK_TAIL;  // see walk()     // waves of 64; each wave starts on one 8x8 pixel tile
 constexpr double kScale = 1 / static_cast<double>(4294967295u - 1);  // rand_util.h:110-112
 
+typedef double Dvec2 __attribute__((ext_vector_type(2)));
+typedef uint32_t Uvec4 __attribute__((ext_vector_type(4)));
+
 struct SceneView {
-    const DevNode* nodes;
-    const DevNode* top_nodes;  // LDS copy of the first ntop (breadth-first) nodes, HBM scenes
-    uint32_t ntop;
+    const DevNode* nodes;      // f64 nodes (HBM): trace(), the walk's EXACT variant and fallback
+    const DevNodeF* fnodes;    // f32 walk nodes (HBM), refs = byte offsets
+    uint32_t ntop;             // HBM-scene kernels: f32 refs below ntop are read from the LDS copy
     const uint32_t* refs;
     const DevSphere* spheres;
+    const DevSpherePair* spair;  // f32 filter records (HBM)
+    uint32_t spair_lds;          // LSCENE kernels: LDS byte offset of the staged copy
     const uint32_t* sphere_mat;
     const DevQuad* quads;
     const uint32_t* quad_mat;
@@ -72,9 +74,12 @@ struct Work {
     uint32_t bytes_nodes, bytes_refs, bytes_spheres, bytes_quads;
     uint32_t sphere_only;   // every primitive is a sphere: refs[slot] == slot
     uint32_t exact_slab;    // the scene needs walk_step's EXACT variant for every ray
-    uint32_t ntop;          // HBM-scene kernels: nodes [0, ntop) staged in LDS at lds_nodes
-    uint32_t sentinel;      // the sentinel node's reference (LDS byte offset for LSCENE kernels)
+    uint32_t ntop;          // HBM-scene kernels: f32 nodes [0, ntop) bytes staged in LDS at offset 0
+    uint32_t sentinel;      // the sentinel node's reference (byte offset into the f32 nodes)
     uint32_t lds_cam;       // LDS copy of the CamView (read where used: keeps it out of SGPRs)
+    uint32_t f32_ok;        // node bounds fit the f32 walk's error analysis (else f64 decides)
+    uint32_t spheres_f32;   // sphere-only scene within the f32 filter's range (two-pass leaves)
+    float tmin32;           // RN32(camera t_min)
 };
 
 struct Counters {
@@ -82,6 +87,7 @@ struct Counters {
     unsigned long long cyc_walk, cyc_leaf, cyc_shade, cyc_total;  // wave cycles (instrumented pass)
     unsigned long long cyc_tail;  // from the wave's first idle lane (chunk done) to its end
     unsigned long long it_walk, it_leaf, it_shade;  // wave iterations (lane utilization)
+    unsigned long long slow_nodes, it_slow;  // node tests decided in f64 (lanes / wave iterations)
 };
 
 // one lane's counts in the instrumented pass (32-bit: a lane handles one sample chunk), added to
@@ -89,6 +95,7 @@ struct Counters {
 struct LaneCounters {
     uint32_t rays, nodes, sphere_tests, quad_tests;
     uint32_t it_walk, it_leaf, it_shade;
+    uint32_t slow_nodes, it_slow;
 };
 
 // counts one per wave: only the lowest active lane increments
@@ -256,31 +263,178 @@ __device__ __forceinline__ bool hit_sphere(const DevSphere& sp, const double o[3
     return true;
 }
 
-// The candidate filter of two-pass sphere leaves: false only when the exact test (hit_sphere,
-// i.e. Sphere::hit_by) provably rejects the sphere for every t_max' <= the t_max behind `hi`.
-// No square root: with y = -b - hi and w = b + lo,
+// v_min/v_max(3)_f32 of non-NaN operands. Written out because fminf/fmaxf make the compiler
+// quieten possible signalling NaNs of operands it cannot prove canonical (tmin', tmax') with an
+// extra v_max each, in every walk step.
+__device__ __forceinline__ float vmin(float a, float b) { float r; asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b)); return r; }
+__device__ __forceinline__ float vmax(float a, float b) { float r; asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b)); return r; }
+__device__ __forceinline__ float vmin3(float a, float b, float c) {
+    float r;
+    asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+// b wave-uniform, in an SGPR
+__device__ __forceinline__ float vmax_s(float a, float b) { float r; asm("v_max_f32 %0, %2, %1" : "=v"(r) : "v"(a), "s"(b)); return r; }
+__device__ __forceinline__ float vmax_abs(float a, float b) {
+    float r;
+    asm("v_max_f32 %0, |%1|, |%2|" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ float vmax3_0(float a, float b) {  // max(a, b, 0)
+    float r;
+    asm("v_max3_f32 %0, %1, %2, 0" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ float vmax3(float a, float b, float c) {
+    float r;
+    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
+// The candidate filter of two-pass sphere leaves, two spheres per step in packed f32
+// (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32: one instruction for both spheres). It returns two
+// bits, false only where the exact test (hit_sphere, i.e. Sphere::hit_by) provably rejects the
+// sphere for every t_max' <= t_max. No square root: with y = -b - hi and w = b + lo,
 //   no real root          <=  D < 0
 //   both roots >= t_max   <=  y > 0 and y^2 > D
 //   both roots <= t_min   <=  w > 0 and w^2 > D
-// where D = disc' + 2^-30 S + 2^-500 bounds the exact test's disc from above: disc' is evaluated
-// with fused multiply-adds, and |disc' - disc| <= 31 u S with S = a (|oc|^2 + r^2) >= |disc| / 2,
-// u = 2^-53 (each of b, |oc|^2, c is within 5u of its exact value in both evaluations). The
-// 2^-30 S slack also covers the error of b' in y and w; lo / hi (lim_tmin / lim_tmax) carry the
-// 2^-30 relative slack for the rounding of the exact roots. NaN or inf anywhere rejects nothing.
-// Valid for a = dot(d, d) in [2^-500, 2^500] (leaf_step checks). tools/fuzz_sphere_filter.c
-// checks it against the exact test on tangent, self-intersecting and wide-range cases.
-__device__ __forceinline__ bool sphere_candidate(const DevSphere& sp, const double o[3], const double d[3],
-                                                 double a, double lo, double hi) {
-    const double ocx = o[0] - sp.c[0], ocy = o[1] - sp.c[1], ocz = o[2] - sp.c[2];
-    const double b = fma(d[2], ocz, fma(d[1], ocy, d[0] * ocx));
-    const double q = fma(ocz, ocz, fma(ocy, ocy, ocx * ocx));
-    const double r2 = sp.r * sp.r;
-    const double disc = fma(b, b, -(a * (q - r2)));
-    const double D = fma(a * (q + r2), 0x1p-30, disc) + 0x1p-500;
-    const double y = -b - hi, w = b + lo;
-    // for D >= 0, "y > 0 and y^2 > D" is y |y| > D
-    const int rej = static_cast<int>(D < 0) | static_cast<int>(y * fabs(y) > D) | static_cast<int>(w * fabs(w) > D);
-    return rej == 0;
+// i.e. reject <=> max(y|y|, w|w|, 0) > D, where D bounds the exact test's discriminant from above
+// with room to spare:
+//   D = b'^2 - a' (q' (1 - 2^-15) - r2e - kap),  b' = d32 . X, q' = X . X, X = o32 - c32,
+//   r2e = RN32(r^2 (1 + 2^-14) + 2^22 |c - c32|^2)  (per sphere, DevSpherePair),
+//   kap = RN32(2^22 |o - o32|^2 + 2^-50)           (per ray),
+// and hi = RN32(t_max a (1 + 2^-20)), lo = RN32(t_min a (1 - 2^-20)). Error budget: with
+// S = a (|oc|^2 + r^2) >= b^2, |disc|, and Delta = |o - o32| + |c - c32| (the rounding of the
+// inputs), every f32 rounding error is below 2^-19 S, and the terms in Delta are at most
+// 4 a |oc| Delta + 2 a Delta^2 <= 2^-17 a |oc|^2 + 2^20 a Delta^2 (AM-GM); the slack of D,
+// 2^-15 a q' + 2^-14 a r^2 + 2^22 a (|o - o32|^2 + |c - c32|^2) >= those, also covers the error of
+// b' inside y and w (2 |y| |b' - b| <= 2^-18 a q + 2^18 a Delta^2), and hi / lo carry a 2^-20
+// relative slack for the rounding of the exact roots (the f64 analysis: 2^-30). A sphere the
+// filter rejects is rejected by the exact test for this t_max and any smaller one, so hits and
+// the tie order are the sequential loop's. Valid for |o_k|, |d_k|, |c_k|, |r| <= 2^30 and
+// a in [2^-60, 2^60] (leaf_step checks; W.spheres_f32 for the scene).
+// tools/fuzz_sphere_filter.c checks the filter (this exact f32 sequence) against the exact test.
+typedef float F2 __attribute__((ext_vector_type(2)));
+// The ray in f32 for the packed filter (per entered leaf), two scalars per register pair; the
+// packed instructions broadcast one half with op_sel / op_sel_hi (no splatted copies: 10 VGPRs
+// instead of 20 while the leaf phase runs).
+struct LeafRay32 {
+    F2 oxy, ozdx, dydz, akap, hilo;  // (ox, oy) (oz, dx) (dy, dz) (a, kap) (hi, lo)
+};
+__device__ __forceinline__ void leaf_ray32(const double o[3], const double d[3], double a, double tmin,
+                                           double tmax, LeafRay32& L) {
+    float o32[3];
+    double e2 = 0;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        o32[k] = static_cast<float>(o[k]);
+        const double e = o[k] - static_cast<double>(o32[k]);
+        e2 = e2 + e * e;
+    }
+    L.oxy = F2{o32[0], o32[1]};
+    L.ozdx = F2{o32[2], static_cast<float>(d[0])};
+    L.dydz = F2{static_cast<float>(d[1]), static_cast<float>(d[2])};
+    L.akap = F2{static_cast<float>(a), static_cast<float>(e2 * 0x1p22 + 0x1p-50)};
+    L.hilo = F2{static_cast<float>(tmax * a * (1 + 0x1p-20)), static_cast<float>(tmin * a * (1 - 0x1p-20))};
+}
+__device__ __forceinline__ bool leaf_ray32_ok(const double o[3], const double d[3], double a) {
+    bool ok = a >= 0x1p-60 && a <= 0x1p60;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) ok = ok && fabs(o[k]) <= 0x1p30 && fabs(d[k]) <= 0x1p30;
+    return ok;
+}
+__device__ __forceinline__ float vmul_abs(float a, float b) {  // a * |b|
+    float r;
+    asm("v_mul_f32 %0, %1, |%2|" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+// packed f32 with one operand broadcast from the low (_L) or high (_H) half of a ray pair p
+__device__ __forceinline__ F2 sub_pL(F2 p, F2 c) {  // (p.x, p.x) - c
+    F2 r;
+    asm("v_pk_add_f32 %0, %1, %2 op_sel_hi:[0,1] neg_lo:[0,1] neg_hi:[0,1]" : "=v"(r) : "v"(p), "v"(c));
+    return r;
+}
+__device__ __forceinline__ F2 sub_pH(F2 p, F2 c) {  // (p.y, p.y) - c
+    F2 r;
+    asm("v_pk_add_f32 %0, %1, %2 op_sel:[1,0] op_sel_hi:[1,1] neg_lo:[0,1] neg_hi:[0,1]" : "=v"(r) : "v"(p), "v"(c));
+    return r;
+}
+__device__ __forceinline__ F2 add_pH(F2 p, F2 c) {  // (p.y, p.y) + c
+    F2 r;
+    asm("v_pk_add_f32 %0, %1, %2 op_sel:[1,0] op_sel_hi:[1,1]" : "=v"(r) : "v"(p), "v"(c));
+    return r;
+}
+__device__ __forceinline__ F2 mul_pL(F2 p, F2 c) {  // (p.x, p.x) * c
+    F2 r;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(r) : "v"(p), "v"(c));
+    return r;
+}
+__device__ __forceinline__ F2 mul_pH(F2 p, F2 c) {  // (p.y, p.y) * c
+    F2 r;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel:[1,0] op_sel_hi:[1,1]" : "=v"(r) : "v"(p), "v"(c));
+    return r;
+}
+__device__ __forceinline__ F2 fma_pL(F2 p, F2 c, F2 e) {  // fma((p.x, p.x), c, e)
+    F2 r;
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1]" : "=v"(r) : "v"(p), "v"(c), "v"(e));
+    return r;
+}
+__device__ __forceinline__ F2 fma_pH(F2 p, F2 c, F2 e) {  // fma((p.y, p.y), c, e)
+    F2 r;
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[1,1,1]" : "=v"(r) : "v"(p), "v"(c), "v"(e));
+    return r;
+}
+__device__ __forceinline__ F2 nsub_pL(F2 b, F2 p) {  // -b - (p.x, p.x)
+    F2 r;
+    asm("v_pk_add_f32 %0, %1, %2 op_sel_hi:[1,0] neg_lo:[1,1] neg_hi:[1,1]" : "=v"(r) : "v"(b), "v"(p));
+    return r;
+}
+__device__ __forceinline__ F2 add_bH(F2 b, F2 p) {  // b + (p.y, p.y)
+    F2 r;
+    asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,1]" : "=v"(r) : "v"(b), "v"(p));
+    return r;
+}
+// records read through explicitly typed LDS / global pointers (a generic pointer would make the
+// compiler emit flat loads), as 16-byte vectors
+typedef float Fvec4 __attribute__((ext_vector_type(4)));
+struct PairLines {
+    Fvec4 c;   // cx0 cx1 cy0 cy1
+    Fvec4 zr;  // cz0 cz1 r2e0 r2e1
+};
+typedef __attribute__((address_space(3))) const PairLines LdsPair;
+typedef __attribute__((address_space(1))) const PairLines GlobalPair;
+template <typename P>
+__device__ __forceinline__ DevSpherePair pair_at(P p) {
+    const Fvec4 c = p->c, zr = p->zr;
+    DevSpherePair r;
+    r.cx[0] = c.x; r.cx[1] = c.y; r.cy[0] = c.z; r.cy[1] = c.w;
+    r.cz[0] = zr.x; r.cz[1] = zr.y; r.r2e[0] = zr.z; r.r2e[1] = zr.w;
+    return r;
+}
+struct SphereLines {
+    Dvec2 a, b;  // (cx, cy), (cz, r)
+};
+typedef __attribute__((address_space(1))) const SphereLines GlobalSphere;
+__device__ __forceinline__ DevSphere sphere_global(const DevSphere* p) {
+    const GlobalSphere* q = (GlobalSphere*)p;
+    const Dvec2 a = q->a, b = q->b;
+    DevSphere r;
+    r.c[0] = a.x; r.c[1] = a.y; r.c[2] = b.x; r.r = b.y;
+    return r;
+}
+// the verdicts of the record's two spheres: bit 1 = first, bit 0 = second (1 = candidate)
+__device__ __forceinline__ uint32_t sphere_pair_candidates(const DevSpherePair& sp, const LeafRay32& L) {
+    const F2 cx = {sp.cx[0], sp.cx[1]}, cy = {sp.cy[0], sp.cy[1]}, cz = {sp.cz[0], sp.cz[1]};
+    const F2 r2e = {sp.r2e[0], sp.r2e[1]};
+    const F2 xx = sub_pL(L.oxy, cx), xy = sub_pH(L.oxy, cy), xz = sub_pL(L.ozdx, cz);
+    const F2 b = fma_pH(L.dydz, xz, fma_pL(L.dydz, xy, mul_pH(L.ozdx, xx)));
+    const F2 q = __builtin_elementwise_fma(xz, xz, __builtin_elementwise_fma(xy, xy, xx * xx));
+    const F2 g = __builtin_elementwise_fma(q, F2{1 - 0x1p-15f, 1 - 0x1p-15f}, -add_pH(L.akap, r2e));
+    const F2 D = __builtin_elementwise_fma(b, b, -mul_pL(L.akap, g));
+    const F2 y = nsub_pL(b, L.hilo), w = add_bH(b, L.hilo);
+    const float m0 = vmax3_0(vmul_abs(y.x, y.x), vmul_abs(w.x, w.x));
+    const float m1 = vmax3_0(vmul_abs(y.y, y.y), vmul_abs(w.y, w.y));
+    return (static_cast<uint32_t>(!(m0 > D.x)) << 1) | static_cast<uint32_t>(!(m1 > D.y));
 }
 
 // Parallelogram::hit_by (parallelogram.h:177-240)
@@ -432,7 +586,11 @@ enum : uint32_t { kWalk = 0, kLeaf = 1, kDone = 2, kIdle = 3 };
 constexpr uint32_t kZeroDir = 8u;
 
 struct Trav {
-    double inv[3];
+    // f32 copies for the walk's node test (walk()): inv32 = RN32(1/d), oinv32 = RN32(o * (1/d)),
+    // marg = the per-ray part of the decision margin (inf: every node test is decided in f64)
+    float inv32[3], oinv32[3];
+    float marg;
+    float tmax32;    // RN32(min(tmax, 2^100))
     double a;        // dot(d, d)
     double tmax;
     uint32_t cur, ref;
@@ -445,61 +603,69 @@ struct Trav {
 
 __device__ __forceinline__ bool finite_nonzero(double x) { return fabs(x) < __builtin_inf() && x != 0; }
 __device__ __forceinline__ bool finite(double x) { return fabs(x) < __builtin_inf(); }
+__device__ __forceinline__ float tmax_f32(double t) { return static_cast<float>(fmin(t, 0x1p100)); }
 
-__device__ __forceinline__ void trav_init(const double o[3], const double d[3], Trav& R) {
-    R.inv[0] = 1 / d[0];
-    R.inv[1] = 1 / d[1];
-    R.inv[2] = 1 / d[2];
+// f32_ok: the scene's node bounds fit the f32 error analysis (Work::f32_ok)
+__device__ __forceinline__ void trav_init(const double o[3], const double d[3], bool f32_ok, Trav& R) {
+    const double inv[3] = {1 / d[0], 1 / d[1], 1 / d[2]};
     R.a = d[0] * d[0] + d[1] * d[1] + d[2] * d[2];
     R.tmax = __builtin_inf();
+    R.tmax32 = 0x1p100f;
     R.cur = 0;
     R.sp = 0;
     R.ref = 0;
-    const bool fast = finite_nonzero(R.inv[0]) && finite_nonzero(R.inv[1]) && finite_nonzero(R.inv[2]) &&
+    const bool fast = finite_nonzero(inv[0]) && finite_nonzero(inv[1]) && finite_nonzero(inv[2]) &&
                       finite(o[0]) && finite(o[1]) && finite(o[2]);
     R.neg = (d[0] < 0 ? 1u : 0u) | (d[1] < 0 ? 2u : 0u) | (d[2] < 0 ? 4u : 0u) | (fast ? 0u : kZeroDir);
+    // the f32 node test's error analysis (walk()) holds for 2^-40 <= |1/d_k| <= 2^40 and
+    // |o_k| <= 2^40; other rays get marg = inf, i.e. every node test decided in f64
+    bool f32 = f32_ok;
+    double A = 0;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const double oi = o[k] * inv[k];
+        R.inv32[k] = static_cast<float>(inv[k]);
+        R.oinv32[k] = static_cast<float>(oi);
+        A = fmax(A, fabs(oi));
+        f32 = f32 && fabs(inv[k]) <= 0x1p40 && fabs(inv[k]) >= 0x1p-40 && fabs(o[k]) <= 0x1p40;
+    }
+    R.marg = f32 ? static_cast<float>(fmax(A * 0x1p-19, 0x1p-60)) : __builtin_inff();
     R.state = kWalk;
     R.found = false;
 }
 
-// one node of the DFS (bvh.h:617-712 loop body without the leaf's primitive loop), branch-free:
-// the node's bounds, index/count/axis/flags and the stack top are loaded in one batch, and the
-// push / pop / leaf / done outcomes are selected rather than branched to (only the push is a
-// masked store).
-// Slab test (aabb.h:141-159). The reference swaps each axis' (t0, t1) by the sign of d and then
-// narrows with "if (y > x) x = y"-style selects; for NaN-free slab values that is exactly
-//   near_k = min(t0_k, t1_k), far_k = max(t0_k, t1_k),
-//   enter  = max(near) <= min(far)  &&  max(near) < tmax  &&  min(far) > tmin
-// (c1 && c2 of the reference <=> every near_i <= far_j; +-0 ties only meet comparisons). A slab
-// value is NaN only for 0 * inf or inf - inf: rays whose inv[] is not finite and nonzero or whose
-// origin is not finite (R.neg & kZeroDir), and scenes with an inverted / NaN node box
-// (Work::exact_slab, where min/max would reorder the axis) take the EXACT variant, the reference's select sequence verbatim
-// with per-lane bound addresses x[neg] / x[!neg].
-// node i of the breadth-first device array: with TOP, the first S.ntop nodes are read from their
-// LDS copy and the rest from HBM (generic loads); otherwise all from S.nodes
-template <bool TOP>
-__device__ __forceinline__ const DevNode* node_at(const SceneView& S, uint32_t i) {
-    if (TOP) return (i < S.ntop ? S.top_nodes : S.nodes) + i;
-    return S.nodes + i;
-}
-
-// A node reference of the render kernel: LS (LDS-staged scene) kernels address nodes by their
-// LDS byte offset (the staged copy holds interior children as byte offsets, stage_nodes_lds), so
-// a node load needs no address arithmetic; the other kernels use node_at.
-// (The LDS pointer is made from the offset itself: the kernel's dynamic LDS starts at LDS
-// address 0, which render_kernel checks, so no base address is added per node.)
+// ---- the render kernel's BVH walk ------------------------------------------------------------
+// One node of the DFS (bvh.h:617-712 loop body without the leaf's primitive loop), branch-free:
+// the node and the stack top are loaded in one batch, and the push / pop / leaf / done outcomes
+// are selected rather than branched to (only the push is a masked store).
+//
+// Node test (AABB::is_hit_by_optimized, aabb.h:132-174). The reference swaps each axis' (t0, t1)
+// by the sign of d and then narrows with "if (y > x) x = y"-style selects; for NaN-free slab
+// values that is exactly
+//   near = max_k min(t0_k, t1_k), far = min_k max(t0_k, t1_k),
+//   enter = near <= far && near < tmax && far > tmin
+// (c1 && c2 of the reference <=> every near_i <= far_j; +-0 ties only meet comparisons), with
+// t_jk = RN(RN(b_jk - o_k) * inv_k) in f64. A slab value is NaN only for 0 * inf or inf - inf:
+// rays whose 1/d is not finite and non-zero or whose origin is not finite (R.neg & kZeroDir), and
+// scenes with an inverted / NaN node box (Work::exact_slab, where min/max would reorder the axis)
+// take the EXACT variant: the reference's select sequence verbatim on the f64 node.
+//
+// The other rays decide the test in f32 first (Trav::inv32 / oinv32 / marg, DevNodeF):
+//   t'_jk = fma(b32_jk, inv32_k, -oinv32_k),  b32 = RN32(b), inv32 = RN32(inv), oinv32 =
+//   RN32(RN(o * inv)). With u = 2^-24 and A = max_k |o_k inv_k|, and |b| <= |b - o| + |o|,
+//   |t' - t| <= 3.01 u (|b| + |o|) |inv| + 2.01 u64 |t| <= 2^-22.4 |t'| + 2^-21.4 A + 2^-85
+// (2^-85: f32 underflow at |inv| <= 2^40). min / max are 1-Lipschitz, so lo' = max(near', tmin')
+// and hi' = min(far', tmax') are within that bound of lo = max(near, tmin), hi = min(far, tmax)
+// with |t'| <= M = max(|lo'|, |hi'|) (tmin', tmax' are RN32 of tmin, tmax; tmax' = 2^100 for
+// larger tmax never binds, as |t'| < 2^82 here), and gap' = RN32(hi' - lo') is within
+// 2^-21 M + 2^-20.4 A + 2^-84 of gap = hi - lo. So with th = 2^-19 M + marg, marg =
+// max(2^-19 A, 2^-60):
+//   gap' >  th  =>  gap > 0: far > near, near < tmax, far > tmin  (enter)
+//   gap' < -th  =>  gap < 0: far < near, far < tmin or tmax < near (no entry)
+// and only lanes with |gap'| <= th (grazing rays, ties, rays with marg = inf) run the f64 test on
+// the f64 node. Every decision is the f64 test's, so each ray visits the reference's node
+// sequence. The f32 test is 18 single-rate instructions where the f64 one is 25 half-rate ones.
 typedef __attribute__((address_space(3))) const unsigned char LdsByte;
-template <bool TOP, bool LS>
-__device__ __forceinline__ const DevNode* node_ref(const SceneView& S, uint32_t cur) {
-    if (LS) return (const DevNode*)(LdsByte*)static_cast<uintptr_t>(cur);
-    return node_at<TOP>(S, cur);
-}
-
-// The four 16-byte lines of node `cur` (see node_ref). TOP kernels read a top-treelet node from
-// LDS and any other from HBM with separate, masked loads into the same registers (no per-lane
-// pointer select, no flat loads).
-typedef double Dvec2 __attribute__((ext_vector_type(2)));
-typedef uint32_t Uvec4 __attribute__((ext_vector_type(4)));
 struct NodeLines {
     Dvec2 b[3];  // (x.min, x.max), (y.min, y.max), (z.min, z.max)
     Uvec4 meta;  // index count axis flags
@@ -511,29 +677,64 @@ __device__ __forceinline__ void node_lines(P p, NodeLines& n) {
     n.b[2] = p->b[2];
     n.meta = p->meta;
 }
-typedef __attribute__((address_space(3))) const NodeLines LdsNode;
 typedef __attribute__((address_space(1))) const NodeLines GlobalNode;
+// the f64 node behind f32 ref `cur`
+__device__ __forceinline__ GlobalNode* node64(const SceneView& S, uint32_t cur) {
+    return (GlobalNode*)(S.nodes + (cur >> kNodeFShift));
+}
+
+// the f64 min/max test of a NaN-free ray (the f32 test's fallback)
+__device__ __forceinline__ bool slab64(GlobalNode* p, const double o[3], const double d[3], double tmin,
+                                       double tmax) {
+    NodeLines nd;
+    node_lines(p, nd);
+    // divided here, in the rare branch: hoisted out of the walk loop, 1/d would hold 6 VGPRs
+    double dx = d[0], dy = d[1], dz = d[2];
+    asm volatile("" : "+v"(dx), "+v"(dy), "+v"(dz));
+    const double inv[3] = {1 / dx, 1 / dy, 1 / dz};
+    const Dvec2 bx = nd.b[0], by = nd.b[1], bz = nd.b[2];
+    const double x0 = (bx.x - o[0]) * inv[0], x1 = (bx.y - o[0]) * inv[0];
+    const double y0 = (by.x - o[1]) * inv[1], y1 = (by.y - o[1]) * inv[1];
+    const double z0 = (bz.x - o[2]) * inv[2], z1 = (bz.y - o[2]) * inv[2];
+    const double near = fmax(fmax(fmin(x0, x1), fmin(y0, y1)), fmin(z0, z1));
+    const double far = fmin(fmin(fmax(x0, x1), fmax(y0, y1)), fmax(z0, z1));
+    return (near <= far) & (near < tmax) & (far > tmin);
+}
+
+// The 32-byte f32 node at ref `cur`: LS kernels hold all nodes in LDS at offset 0 (the LDS
+// pointer is the ref itself: render_kernel checks that its dynamic LDS starts at address 0),
+// TOP kernels the first S.ntop bytes of them; the rest is read from HBM, with a separate masked
+// load into the same registers (no per-lane pointer select, no flat loads).
+struct NodeF {
+    Uvec4 q0;  // x.min x.max y.min y.max (f32 bits)
+    Uvec4 q1;  // z.min z.max w0 w1
+};
+typedef __attribute__((address_space(3))) const NodeF LdsNodeF;
+typedef __attribute__((address_space(1))) const NodeF GlobalNodeF;
 template <bool TOP, bool LS>
-__device__ __forceinline__ void fetch_node(const SceneView& S, uint32_t cur, NodeLines& n) {
-    if (LS) {
-        node_lines((LdsNode*)static_cast<uintptr_t>(cur), n);
-    } else if (TOP && cur < S.ntop) {  // the treelet sits at LDS offset 0 (render_kernel checks)
-        node_lines((LdsNode*)static_cast<uintptr_t>(cur * static_cast<uint32_t>(sizeof(DevNode))), n);
+__device__ __forceinline__ void fetch_nodef(const SceneView& S, uint32_t cur, Uvec4& q0, Uvec4& q1) {
+    if (LS || (TOP && cur < S.ntop)) {
+        LdsNodeF* p = (LdsNodeF*)static_cast<uintptr_t>(cur);
+        q0 = p->q0;
+        q1 = p->q1;
     } else {
-        node_lines((GlobalNode*)(S.nodes + cur), n);
+        GlobalNodeF* p = (GlobalNodeF*)(reinterpret_cast<const char*>(S.fnodes) + cur);
+        q0 = p->q0;
+        q1 = p->q1;
     }
 }
 
 template <typename SE, bool COUNT, bool EXACT, bool TOP, bool LS, bool GS>
-__device__ __forceinline__ void walk(const SceneView& S, Stack<SE>& st, const double o[3],
-                                     double tmin, Trav& R, LaneCounters& ctr) {
+__device__ __forceinline__ void walk(const SceneView& S, Stack<SE>& st, const double o[3], const double d[3],
+                                     double tmin, float tmin32, Trav& R, LaneCounters& ctr) {
     // Every step ends with the next node in `cur`: the near child of an entered interior node,
     // else the stack top, popped. The level below the stack holds the sentinel node, entered by
     // every ray, so popping an empty stack leads to the sentinel and the only exit is "entered a
     // node with primitives" (a leaf, or the sentinel: traversal over). An entered leaf ends the
     // walk already popped (the reference pops right after the leaf's primitive loop, which leaves
     // the stack unchanged); its primitive range goes to leaf_step in R.first / R.count. So the
-    // loop body has no branch but that exit, and every lane makes the same updates.
+    // loop body has no branch but that exit (and the rare f64 decision), and every lane makes
+    // the same updates.
     // The stack is walked with a pointer to its top level (level sp - 1). The far child is stored
     // at level sp whatever the outcome (above the live stack unless it is pushed; the stack has
     // depth + 1 levels); at the sentinel that store rewrites the guard level with the sentinel's
@@ -543,69 +744,93 @@ __device__ __forceinline__ void walk(const SceneView& S, Stack<SE>& st, const do
     SE* const empty = st.base - stride;
     SE* tp = st.base + (static_cast<ptrdiff_t>(R.sp) - 1) * stride;
     uint32_t cur = R.cur;
-    uint4 meta;
+    uint32_t w0, w1;  // the last node's DevNodeF words (leaf / sentinel at the exit)
     bool stop;
-    do {
-        NodeLines nd;
-        fetch_node<TOP, LS>(S, cur, nd);
-        meta = make_uint4(nd.meta.x, nd.meta.y, nd.meta.z, nd.meta.w);  // index count axis flags
-        const uint32_t top = *tp;                         // speculative pop
-        if (COUNT) {
-            if (meta.y != kSentinelCount) ctr.nodes++;
-            if (wave_leader()) ctr.it_walk++;
-        }
-        bool enter;
-        if (!EXACT) {
-            // linear-mode nodes (kNodeAlways) and the sentinel carry [-inf, inf] bounds in the
-            // device copy: with finite o and finite non-zero inv every slab is (-inf, inf), so
-            // they are entered
-            const Dvec2 bx = nd.b[0], by = nd.b[1], bz = nd.b[2];
-            const double x0 = (bx.x - o[0]) * R.inv[0], x1 = (bx.y - o[0]) * R.inv[0];
-            const double y0 = (by.x - o[1]) * R.inv[1], y1 = (by.y - o[1]) * R.inv[1];
-            const double z0 = (bz.x - o[2]) * R.inv[2], z1 = (bz.y - o[2]) * R.inv[2];
-            const double near = fmax(fmax(fmin(x0, x1), fmin(y0, y1)), fmin(z0, z1));
-            const double far = fmin(fmin(fmax(x0, x1), fmax(y0, y1)), fmax(z0, z1));
-            enter = (near <= far) & (near < R.tmax) & (far > tmin);
-        } else {
+    if (EXACT) {
+        const double inv[3] = {1 / d[0], 1 / d[1], 1 / d[2]};
+        do {
+            NodeLines nd;
+            node_lines(node64(S, cur), nd);
+            const Uvec4 meta = nd.meta;  // index count axis flags
+            const uint32_t top = *tp;    // speculative pop
+            if (COUNT) {
+                if (meta.y != kSentinelCount) ctr.nodes++;
+                if (wave_leader()) ctr.it_walk++;
+            }
             // x[neg] / x[!neg]
             const bool nx = R.neg & 1u, ny = (R.neg >> 1) & 1u, nz = (R.neg >> 2) & 1u;
             const double bx0 = nx ? nd.b[0].y : nd.b[0].x, bx1 = nx ? nd.b[0].x : nd.b[0].y;
             const double by0 = ny ? nd.b[1].y : nd.b[1].x, by1 = ny ? nd.b[1].x : nd.b[1].y;
             const double bz0 = nz ? nd.b[2].y : nd.b[2].x, bz1 = nz ? nd.b[2].x : nd.b[2].y;
-            double xtmin = (bx0 - o[0]) * R.inv[0];
-            double xtmax = (bx1 - o[0]) * R.inv[0];
-            const double ytmin = (by0 - o[1]) * R.inv[1];
-            const double ytmax = (by1 - o[1]) * R.inv[1];
-            const double ztmin = (bz0 - o[2]) * R.inv[2];
-            const double ztmax = (bz1 - o[2]) * R.inv[2];
+            double xtmin = (bx0 - o[0]) * inv[0];
+            double xtmax = (bx1 - o[0]) * inv[0];
+            const double ytmin = (by0 - o[1]) * inv[1];
+            const double ytmax = (by1 - o[1]) * inv[1];
+            const double ztmin = (bz0 - o[2]) * inv[2];
+            const double ztmax = (bz1 - o[2]) * inv[2];
             const bool c1 = !(xtmin > ytmax || ytmin > xtmax);
             if (ytmin > xtmin) xtmin = ytmin;
             if (ytmax < xtmax) xtmax = ytmax;
             const bool c2 = !(xtmin > ztmax || ztmin > xtmax);
             if (ztmin > xtmin) xtmin = ztmin;
             if (ztmax < xtmax) xtmax = ztmax;
-            enter = (c1 & c2 & (xtmin < R.tmax) & (xtmax > tmin)) |
-                    (meta.y != 0 && (meta.w & kNodeAlways) != 0) | (meta.y == kSentinelCount);
-        }
-        const bool inner = enter & (meta.y == 0);
-        const bool far_first = (R.neg >> meta.z) & 1u;
-        const uint32_t near_child = far_first ? meta.x : meta.w;  // children: left = flags, right = index
-        const uint32_t far_child = far_first ? meta.w : meta.x;
-        tp[stride] = static_cast<SE>(far_child);
-        stop = enter ^ inner;  // entered, not interior: a leaf or the sentinel
-        cur = inner ? near_child : top;
-        tp += inner ? stride : -stride;
-        // once at most kWalkTail lanes still walk, they pause (state stays WALK) and the wave
-        // moves on to the leaf phase; they resume in the next round
-        if (kWalkTail > 0 && !stop && __popcll(__ballot(1)) <= kWalkTail) {
-            R.cur = cur;
-            R.sp = static_cast<int32_t>(static_cast<uint32_t>(tp - empty) / st.stride);
-            return;
-        }
-    } while (!stop);
-    R.state = meta.y == kSentinelCount ? kDone : kLeaf;
-    R.first = meta.x;
-    R.count = meta.y;
+            const bool enter = (c1 & c2 & (xtmin < R.tmax) & (xtmax > tmin)) |
+                               (meta.y != 0 && (meta.w & kNodeAlways) != 0) | (meta.y == kSentinelCount);
+            const bool inner = enter & (meta.y == 0);
+            const bool far_first = (R.neg >> meta.z) & 1u;
+            const uint32_t left = meta.w << kNodeFShift, right = meta.x << kNodeFShift;
+            tp[stride] = static_cast<SE>(far_first ? left : right);
+            stop = enter ^ inner;  // entered, not interior: a leaf or the sentinel
+            cur = inner ? (far_first ? right : left) : top;
+            tp += inner ? stride : -stride;
+            w0 = meta.x;
+            w1 = meta.y == kSentinelCount ? kSentinelW1 : (kLeafFlagF | meta.y);
+        } while (!stop);
+    } else {
+        do {
+            Uvec4 q0, q1;
+            fetch_nodef<TOP, LS>(S, cur, q0, q1);
+            w0 = q1.z;
+            w1 = q1.w;
+            const uint32_t top = *tp;  // speculative pop
+            if (COUNT) {
+                if (w1 != kSentinelW1) ctr.nodes++;
+                if (wave_leader()) ctr.it_walk++;
+            }
+            // the sentinel and linear-mode leaves carry [-inf, inf] boxes: entered (lo' = tmin',
+            // hi' = tmax')
+            const float x0 = __builtin_fmaf(__uint_as_float(q0.x), R.inv32[0], -R.oinv32[0]);
+            const float x1 = __builtin_fmaf(__uint_as_float(q0.y), R.inv32[0], -R.oinv32[0]);
+            const float y0 = __builtin_fmaf(__uint_as_float(q0.z), R.inv32[1], -R.oinv32[1]);
+            const float y1 = __builtin_fmaf(__uint_as_float(q0.w), R.inv32[1], -R.oinv32[1]);
+            const float z0 = __builtin_fmaf(__uint_as_float(q1.x), R.inv32[2], -R.oinv32[2]);
+            const float z1 = __builtin_fmaf(__uint_as_float(q1.y), R.inv32[2], -R.oinv32[2]);
+            const float lo = vmax3(vmin(x0, x1), vmin(y0, y1), vmax_s(vmin(z0, z1), tmin32));
+            const float hi = vmin3(vmax(x0, x1), vmax(y0, y1), vmin(vmax(z0, z1), R.tmax32));
+            const float gap = hi - lo;
+            const float th = __builtin_fmaf(vmax_abs(lo, hi), 0x1p-19f, R.marg);
+            bool enter = gap > 0.f;
+            const bool unc = !(fabsf(gap) > th);
+            if (__builtin_expect(__ballot(unc) != 0, 0)) {
+                if (COUNT && wave_leader()) ctr.it_slow++;
+                if (unc) {
+                    if (COUNT) ctr.slow_nodes++;
+                    enter = slab64(node64(S, cur), o, d, tmin, R.tmax);
+                }
+            }
+            const bool inner = enter & (w1 < kLeafFlagF);
+            // v_bfe_u32 takes the offset from w0's low five bits: the split axis
+            const bool far_first = __builtin_amdgcn_ubfe(R.neg, w0, 1) != 0;
+            const uint32_t right = w0 & ~((1u << kNodeFShift) - 1);
+            tp[stride] = static_cast<SE>(far_first ? w1 : right);
+            stop = enter ^ inner;  // entered, not interior: a leaf or the sentinel
+            cur = inner ? (far_first ? right : w1) : top;
+            tp += inner ? stride : -stride;
+        } while (!stop);
+    }
+    R.state = w1 == kSentinelW1 ? kDone : kLeaf;
+    R.first = w0;
+    R.count = w1 & ~kLeafFlagF;
     R.cur = cur;
     // levels in use after the pop; -1 when the leaf was entered with an empty stack
     R.sp = static_cast<int32_t>(static_cast<uint32_t>(tp - empty)) / static_cast<int32_t>(st.stride);
@@ -616,45 +841,45 @@ __device__ __forceinline__ void walk(const SceneView& S, Stack<SE>& st, const do
 // sphere is loaded while the current one is tested.
 template <typename SE, bool COUNT, bool TOP, bool LS>
 __device__ __forceinline__ void leaf_step(const SceneView& S, Stack<SE>& st, const double o[3],
-                                          const double d[3], double tmin, bool sphere_only,
+                                          const double d[3], double tmin, bool sphere_only, bool pairs,
                                           Trav& R, LaneCounters& ctr) {
     const uint2 range = make_uint2(R.first, R.count);  // index, count
     const uint32_t end = range.x + range.y;
     const double ia = recip_a(R.a), lo = lim_tmin(tmin, R.a);
     double hi = lim_tmax(R.tmax, R.a);
-    if (sphere_only && range.y <= 32 && R.a >= 0x1p-500 && R.a <= 0x1p500) {
-        // two passes: the cheap candidate test of every sphere against the leaf-entry t_max, then
-        // the full test of the candidates in slot order with the shrinking t_max. A sphere the
-        // first pass rejects is rejected by the full test for any smaller t_max too, so the hits
-        // and the tie order are the sequential loop's; the full-test pass runs only as often as
-        // the lane with most candidates needs (typically 1-3 of 6-12).
-        // Pass 1 runs over pairs (the loads of one half overlap the tests of the other, with no
-        // register rotation) and shifts each verdict into `cand`: after the pass, bit
-        // nbits - 1 - i stands for sphere i (nbits = count rounded up to even; the odd count's
-        // extra test reads the slot after the leaf, inside the scene copy, and is masked off).
+    if (pairs && range.y <= 32 && leaf_ray32_ok(o, d, R.a)) {
+        // two passes: the packed f32 candidate filter over every sphere against the leaf-entry
+        // t_max, then the full test of the candidates in slot order with the shrinking t_max. A
+        // sphere the first pass rejects is rejected by the full test for any smaller t_max too,
+        // so the hits and the tie order are the sequential loop's; the full-test pass runs only
+        // as often as the lane with most candidates needs (typically 1-3 of 6-12).
+        // Pass 1 reads pair records (slots first + i, first + i + 1) and shifts both verdicts
+        // into `cand`: after the pass, bit nbits - 1 - i stands for sphere i (nbits = count
+        // rounded up to even; an odd count's extra verdict, for the slot after the leaf, is
+        // masked off).
+        LeafRay32 L;
+        leaf_ray32(o, d, R.a, tmin, R.tmax, L);
         uint32_t cand = 0;
         const uint32_t nbits = (range.y + 1) & ~1u;
-        DevSphere s0 = S.spheres[range.x];
         for (uint32_t i = 0; i < range.y; i += 2) {
-            const DevSphere s1 = S.spheres[range.x + i + 1];
             if (COUNT) {
                 ctr.sphere_tests += i + 1 < range.y ? 2 : 1;
                 if (wave_leader()) ctr.it_leaf += 2;
             }
-            cand = (cand << 1) | static_cast<uint32_t>(sphere_candidate(s0, o, d, R.a, lo, hi));
-            s0 = S.spheres[range.x + i + 2];
-            cand = (cand << 1) | static_cast<uint32_t>(sphere_candidate(s1, o, d, R.a, lo, hi) & (i + 1 < range.y));
+            const DevSpherePair rec = LS ? pair_at((LdsPair*)static_cast<uintptr_t>(S.spair_lds + ((range.x + i) << 5)))
+                                         : pair_at((GlobalPair*)(S.spair + range.x + i));
+            cand = (cand << 2) | sphere_pair_candidates(rec, L);
         }
+        cand &= ~(range.y & 1u);  // an odd count's last verdict is the slot after the leaf
         while (cand) {
             const uint32_t b = 31 - __builtin_clz(cand);
             cand ^= 1u << b;
             const uint32_t i = range.x + (nbits - 1 - b);
             double t;
-#ifndef CRT_P2_COARSE
-#define CRT_P2_COARSE 0
-#endif
-            if (hit_sphere<CRT_P2_COARSE != 0>(S.spheres[i], o, d, R.a, ia, tmin, R.tmax, lo, hi, t)) {
+            // the f64 spheres are in HBM (L1) in this mode
+            if (hit_sphere<false>(sphere_global(S.spheres + i), o, d, R.a, ia, tmin, R.tmax, lo, hi, t)) {
                 R.tmax = t;
+                R.tmax32 = tmax_f32(t);
                 hi = lim_tmax(t, R.a);
                 R.ref = i;
                 R.found = true;
@@ -673,6 +898,7 @@ __device__ __forceinline__ void leaf_step(const SceneView& S, Stack<SE>& st, con
             double t;
             if (hit_sphere(cur, o, d, R.a, ia, tmin, R.tmax, lo, hi, t)) {
                 R.tmax = t;
+                R.tmax32 = tmax_f32(t);
                 hi = lim_tmax(t, R.a);
                 R.ref = i;
                 R.found = true;
@@ -694,6 +920,7 @@ __device__ __forceinline__ void leaf_step(const SceneView& S, Stack<SE>& st, con
             }
             if (h) {
                 R.tmax = t;
+                R.tmax32 = tmax_f32(t);
                 hi = lim_tmax(t, R.a);
                 R.ref = ref;
                 R.found = true;
@@ -850,22 +1077,6 @@ __device__ __forceinline__ void stage_lds(unsigned char* dst, const void* src, u
     for (uint32_t i = threadIdx.x; i < bytes / 16; i += kBlock) d[i] = s[i];
 }
 
-// the node array staged at LDS offset 0 with interior children (count == 0: left = flags, right =
-// index) and the sentinel's self references rewritten as byte offsets, the node references of LS
-// kernels (node_ref)
-__device__ __forceinline__ void stage_nodes_lds(unsigned char* dst, const DevNode* src, uint32_t bytes) {
-    const uint4* s = reinterpret_cast<const uint4*>(src);
-    uint4* d = reinterpret_cast<uint4*>(dst);
-    for (uint32_t i = threadIdx.x; i < bytes / 16; i += kBlock) {
-        uint4 v = s[i];
-        if ((i & 3u) == 3u && (v.y == 0 || v.y == kSentinelCount)) {
-            v.x *= static_cast<uint32_t>(sizeof(DevNode));
-            v.w *= static_cast<uint32_t>(sizeof(DevNode));
-        }
-        d[i] = v;
-    }
-}
-
 // The render kernel. Thread -> (sample chunk, pixel); each wave starts on one 8x8 pixel tile.
 // Persistent per-lane state machine (WALK -> LEAF -> ... -> DONE -> shade -> WALK) in traversal
 // rounds: every walking lane walks the DFS to its next entered leaf (or the end of its
@@ -875,8 +1086,10 @@ __device__ __forceinline__ void stage_nodes_lds(unsigned char* dst, const DevNod
 // runs with many lanes active, and a wave is never held by its slowest ray or path.
 // Samples are summed in sample order into partial[chunk][pixel].
 // LSCENE: nodes, primitive refs, spheres and parallelograms are staged in LDS first.
+// 4 waves per SIMD (128 VGPRs): the f32 walk / packed sphere filter state does not fit 96
+// VGPRs without ~66 spills (5 waves: 3932 vs 4158 Msamples/s on config 2)
 #ifndef CRT_WAVES_PER_EU
-#define CRT_WAVES_PER_EU 5
+#define CRT_WAVES_PER_EU 4
 #endif
 #ifndef CRT_SHADE_BATCH
 #define CRT_SHADE_BATCH 32
@@ -894,21 +1107,26 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRT_WAVE
     Counters* __restrict__ counters) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     SceneView S = Sg;
-    if (LSCENE) {  // nodes at LDS offset 0 (node_ref: a node's LDS address is its byte offset)
+    if (LSCENE) {  // f32 nodes at LDS offset 0 (fetch_nodef: a node's LDS address is its ref)
         if (static_cast<uint32_t>(reinterpret_cast<uintptr_t>((LdsByte*)smem)) != 0) __builtin_trap();
-        stage_nodes_lds(smem, Sg.nodes, W.bytes_nodes);
-        stage_lds(smem + W.lds_refs, Sg.refs, W.bytes_refs);
-        stage_lds(smem + W.lds_spheres, Sg.spheres, W.bytes_spheres);
+        stage_lds(smem, Sg.fnodes, W.bytes_nodes);
         stage_lds(smem + W.lds_quads, Sg.quads, W.bytes_quads);
-        S.nodes = reinterpret_cast<const DevNode*>(smem);
-        S.refs = reinterpret_cast<const uint32_t*>(smem + W.lds_refs);
-        S.spheres = reinterpret_cast<const DevSphere*>(smem + W.lds_spheres);
         S.quads = reinterpret_cast<const DevQuad*>(smem + W.lds_quads);
+        if (W.spheres_f32) {
+            // sphere-only: the filter's pair records in LDS; refs are unused (slot = sphere),
+            // and the f64 spheres (candidates' exact tests, shading) stay in HBM / L1
+            stage_lds(smem + W.lds_spheres, Sg.spair, W.bytes_spheres);
+            S.spair_lds = W.lds_spheres;
+        } else {
+            stage_lds(smem + W.lds_refs, Sg.refs, W.bytes_refs);
+            stage_lds(smem + W.lds_spheres, Sg.spheres, W.bytes_spheres);
+            S.refs = reinterpret_cast<const uint32_t*>(smem + W.lds_refs);
+            S.spheres = reinterpret_cast<const DevSphere*>(smem + W.lds_spheres);
+        }
         __syncthreads();
-    } else if (W.ntop) {  // HBM scene: keep its top ntop nodes (breadth-first) in LDS
+    } else if (W.ntop) {  // HBM scene: keep the first ntop bytes of f32 nodes (top levels) in LDS
         if (static_cast<uint32_t>(reinterpret_cast<uintptr_t>((LdsByte*)smem)) != 0) __builtin_trap();
-        stage_lds(smem + W.lds_nodes, Sg.nodes, W.ntop * static_cast<uint32_t>(sizeof(DevNode)));
-        S.top_nodes = reinterpret_cast<const DevNode*>(smem + W.lds_nodes);
+        stage_lds(smem, Sg.fnodes, W.ntop);
         S.ntop = W.ntop;
         __syncthreads();
     }
@@ -917,6 +1135,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRT_WAVE
     if (threadIdx.x == 0) *reinterpret_cast<CamView*>(smem + W.lds_cam) = C;
     __syncthreads();
     const CamView& CL = *reinterpret_cast<const CamView*>(smem + W.lds_cam);
+    const float tmin32 = W.tmin32;  // a kernel argument (SGPR): no conversion in the walk loop
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t wave = (static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x) >> 6;
     // tile-major: the chunks of one 8x8 tile are consecutive waves, so the four waves of a block
@@ -952,7 +1171,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRT_WAVE
     // max_depth == 0: ray_color returns RGB::zero() for every sample (camera.h:211-213)
     if (valid && C.max_depth > 0 && s < s_end) {
         start_path(CL, row, col, sample_seed(C.base_seed, pixel, s), P);
-        trav_init(P.o, P.d, R);
+        trav_init(P.o, P.d, W.f32_ok != 0, R);
         if (COUNT) ctr.rays++;
     }
     uint32_t cw = 0, cl = 0, cs = 0;  // wall_clock64 ticks (100 MHz), differences mod 2^32
@@ -963,13 +1182,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRT_WAVE
         while (true) {
             if (COUNT) cw -= static_cast<uint32_t>(wall_clock64());
             if (!W.exact_slab && __ballot(R.state == kWalk && (R.neg & kZeroDir)) == 0) {
-                if (R.state == kWalk) walk<SE, COUNT, false, kTopTreelet && !LSCENE, LSCENE, GSTACK>(S, st, P.o, C.t_min, R, ctr);
+                if (R.state == kWalk) walk<SE, COUNT, false, kTopTreelet && !LSCENE, LSCENE, GSTACK>(S, st, P.o, P.d, C.t_min, tmin32, R, ctr);
             } else {
-                if (R.state == kWalk) walk<SE, COUNT, true, kTopTreelet && !LSCENE, LSCENE, GSTACK>(S, st, P.o, C.t_min, R, ctr);
+                if (R.state == kWalk) walk<SE, COUNT, true, kTopTreelet && !LSCENE, LSCENE, GSTACK>(S, st, P.o, P.d, C.t_min, tmin32, R, ctr);
             }
             if (COUNT) cw += static_cast<uint32_t>(wall_clock64());
             if (COUNT) cl -= static_cast<uint32_t>(wall_clock64());
-            if (R.state == kLeaf) leaf_step<SE, COUNT, kTopTreelet && !LSCENE, LSCENE>(S, st, P.o, P.d, C.t_min, W.sphere_only != 0, R, ctr);
+            if (R.state == kLeaf) leaf_step<SE, COUNT, kTopTreelet && !LSCENE, LSCENE>(S, st, P.o, P.d, C.t_min, W.sphere_only != 0, W.spheres_f32 != 0, R, ctr);
             if (COUNT) cl += static_cast<uint32_t>(wall_clock64());
             const uint64_t pending = __ballot(R.state == kWalk);
             const uint64_t finished = __ballot(R.state == kDone);
@@ -990,7 +1209,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRT_WAVE
                     else start_path(CL, row, col, sample_seed(C.base_seed, pixel, s), P);
                 }
                 if (R.state != kIdle) {
-                    trav_init(P.o, P.d, R);
+                    trav_init(P.o, P.d, W.f32_ok != 0, R);
                     if (COUNT) ctr.rays++;
                 }
             }
@@ -1022,6 +1241,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRT_WAVE
         atomicAdd(&counters->it_walk, static_cast<ull>(ctr.it_walk));
         atomicAdd(&counters->it_leaf, static_cast<ull>(ctr.it_leaf));
         atomicAdd(&counters->it_shade, static_cast<ull>(ctr.it_shade));
+        atomicAdd(&counters->slow_nodes, static_cast<ull>(ctr.slow_nodes));
+        atomicAdd(&counters->it_slow, static_cast<ull>(ctr.it_slow));
     }
 }
 
@@ -1122,7 +1343,7 @@ __global__ __launch_bounds__(kBlock) void hits_kernel(SceneView S, const double*
 // host launch plumbing
 
 static dev::SceneView view_of(const DeviceCopy& c) {
-    return dev::SceneView{c.nodes, nullptr, 0, c.refs, c.spheres, c.sphere_mat, c.quads, c.quad_mat, c.mats};
+    return dev::SceneView{c.nodes, c.fnodes, 0, c.refs, c.spheres, c.spair, 0, c.sphere_mat, c.quads, c.quad_mat, c.mats};
 }
 
 int device_count(int* n) {
@@ -1163,10 +1384,60 @@ int device_upload(crt_scene* s, int device) {
     // ref -> primitive map the hit queries report with.
     const size_t n_nodes = s->dnodes.size(), n_refs = s->refs.size();
     const size_t n_sp = s->spheres.size(), n_q = s->quads.size(), n_m = s->dmats.size();
+    // f32 refs are byte offsets (index << 5) and interior w1 must stay below kLeafFlagF
+    if (n_nodes >= (size_t{1} << (31 - kNodeFShift)))
+        return fail(CRT_E_INVALID, "BVH too large for the device node layout");
+    std::vector<DevNodeF> fnodes(n_nodes);
+    bool f32_ok = true;
+    for (size_t i = 0; i < n_nodes; ++i) {
+        const DevNode& n = s->dnodes[i];
+        DevNodeF& f = fnodes[i];
+        for (int k = 0; k < 6; ++k) {
+            f.b[k] = static_cast<float>(n.b[k]);  // round to nearest
+            if (!std::isinf(n.b[k]) && !(std::fabs(n.b[k]) <= kF32BoundMax)) f32_ok = false;
+        }
+        if (n.count == 0) {
+            f.w0 = (n.index << kNodeFShift) | n.axis;
+            f.w1 = n.flags << kNodeFShift;
+        } else if (n.count == kSentinelCount) {
+            // "axis" 3: R.neg bit 3 (kZeroDir) is clear in the f32 walk, so the far child the
+            // walk stores at the sentinel (into the guard level) is w0 & ~31, the sentinel itself
+            f.w0 = (static_cast<uint32_t>(i) << kNodeFShift) | 3u;
+            f.w1 = kSentinelW1;
+        } else {
+            f.w0 = n.index;
+            f.w1 = kLeafFlagF | n.count;
+        }
+    }
     size_t off_nodes = 0;
-    size_t off_refs = align256(off_nodes + n_nodes * sizeof(DevNode));
+    size_t off_fnodes = align256(off_nodes + n_nodes * sizeof(DevNode));
+    // sphere pair records of the f32 candidate filter (slots i, i + 1)
+    std::vector<DevSpherePair> spair(n_sp);
+    bool spheres_f32_ok = true;
+    for (size_t i = 0; i < n_sp; ++i) {
+        const DevSphere& sp = s->spheres[i];
+        double dc2 = 0;
+        for (int k = 0; k < 3; ++k) {
+            if (!(std::fabs(sp.c[k]) <= kF32SphereMax)) spheres_f32_ok = false;
+            const double e = sp.c[k] - static_cast<double>(static_cast<float>(sp.c[k]));
+            dc2 += e * e;
+        }
+        if (!(std::fabs(sp.r) <= kF32SphereMax)) spheres_f32_ok = false;
+        const float cx = static_cast<float>(sp.c[0]), cy = static_cast<float>(sp.c[1]), cz = static_cast<float>(sp.c[2]);
+        const float r2e = static_cast<float>(sp.r * sp.r * (1 + 0x1p-14) + dc2 * 0x1p22);
+        spair[i].cx[0] = cx; spair[i].cy[0] = cy; spair[i].cz[0] = cz; spair[i].r2e[0] = r2e;
+        if (i > 0) {
+            spair[i - 1].cx[1] = cx; spair[i - 1].cy[1] = cy; spair[i - 1].cz[1] = cz; spair[i - 1].r2e[1] = r2e;
+        }
+    }
+    if (n_sp) {
+        DevSpherePair& last = spair[n_sp - 1];
+        last.cx[1] = last.cy[1] = last.cz[1] = last.r2e[1] = 0;
+    }
+    size_t off_refs = align256(off_fnodes + n_nodes * sizeof(DevNodeF));
     size_t off_sp = align256(off_refs + n_refs * 4);
-    size_t off_spm = align256(off_sp + n_sp * sizeof(DevSphere));
+    size_t off_spp = align256(off_sp + n_sp * sizeof(DevSphere));
+    size_t off_spm = align256(off_spp + n_sp * sizeof(DevSpherePair));
     size_t off_q = align256(off_spm + n_sp * 4);
     size_t off_qm = align256(off_q + n_q * sizeof(DevQuad));
     size_t off_m = align256(off_qm + n_q * 4);
@@ -1180,8 +1451,10 @@ int device_upload(crt_scene* s, int device) {
     };
     hipError_t e = hipSuccess;
     if (e == hipSuccess) e = up(off_nodes, s->dnodes.data(), n_nodes * sizeof(DevNode));
+    if (e == hipSuccess) e = up(off_fnodes, fnodes.data(), n_nodes * sizeof(DevNodeF));
     if (e == hipSuccess) e = up(off_refs, s->refs.data(), n_refs * 4);
     if (e == hipSuccess) e = up(off_sp, s->spheres.data(), n_sp * sizeof(DevSphere));
+    if (e == hipSuccess) e = up(off_spp, spair.data(), n_sp * sizeof(DevSpherePair));
     if (e == hipSuccess) e = up(off_spm, s->sphere_mat.data(), n_sp * 4);
     if (e == hipSuccess) e = up(off_q, s->quads.data(), n_q * sizeof(DevQuad));
     if (e == hipSuccess) e = up(off_qm, s->quad_mat.data(), n_q * 4);
@@ -1193,8 +1466,12 @@ int device_upload(crt_scene* s, int device) {
     c.base = base;
     c.bytes = total;
     c.nodes = reinterpret_cast<DevNode*>(b + off_nodes);
+    c.fnodes = reinterpret_cast<DevNodeF*>(b + off_fnodes);
+    c.f32_ok = f32_ok && std::getenv("CRT_F64_NODES") == nullptr;
     c.refs = reinterpret_cast<uint32_t*>(b + off_refs);
     c.spheres = reinterpret_cast<DevSphere*>(b + off_sp);
+    c.spair = reinterpret_cast<DevSpherePair*>(b + off_spp);
+    c.spheres_f32_ok = spheres_f32_ok && std::getenv("CRT_F64_SPHERES") == nullptr;
     c.sphere_mat = reinterpret_cast<uint32_t*>(b + off_spm);
     c.quads = reinterpret_cast<DevQuad*>(b + off_q);
     c.quad_mat = reinterpret_cast<uint32_t*>(b + off_qm);
@@ -1336,6 +1613,8 @@ static int launch_render(const crt_scene* s, int device, const crt_camera* cam, 
         count_stats->wave_iters_leaf = h.it_leaf;
         count_stats->wave_iters_shade = h.it_shade;
         count_stats->ticks_tail = h.cyc_tail;
+        count_stats->slow_node_tests = h.slow_nodes;
+        count_stats->wave_iters_slow = h.it_slow;
         if (std::getenv("CRT_DEBUG_COUNTERS"))
             std::fprintf(stderr, "crt counters: rays %llu nodes %llu sphere_tests %llu quad_tests %llu it_walk %llu "
                          "it_leaf %llu it_shade %llu\n", h.rays, h.nodes, h.sphere_tests, h.quad_tests, h.it_walk,
@@ -1351,13 +1630,18 @@ static int dispatch_render(const crt_scene* s, int device, const crt_camera* cam
                            double* d_rgb, hipStream_t st, crt_render_stats* count_stats) {
     // depth + 1 levels: walk_step stores the far child at level sp unconditionally
     const size_t stack_bytes = align16(static_cast<size_t>(s->depth + 1) * dev::kBlock * sizeof(SE));
-    W.bytes_nodes = static_cast<uint32_t>(align16(s->dnodes.size() * sizeof(DevNode)));
-    W.bytes_refs = static_cast<uint32_t>(align16(s->refs.size() * 4));
-    W.bytes_spheres = static_cast<uint32_t>(align16(s->spheres.size() * sizeof(DevSphere)));
+    W.bytes_nodes = static_cast<uint32_t>(align16(s->dnodes.size() * sizeof(DevNodeF)));
+    // sphere-only scenes in f32 range stage the filter's pair records instead of refs + spheres
+    W.bytes_refs = W.spheres_f32 ? 0u : static_cast<uint32_t>(align16(s->refs.size() * 4));
+    W.bytes_spheres = static_cast<uint32_t>(align16(s->spheres.size() * (W.spheres_f32 ? sizeof(DevSpherePair)
+                                                                                         : sizeof(DevSphere))));
     W.bytes_quads = static_cast<uint32_t>(align16(s->quads.size() * sizeof(DevQuad)));
     const size_t scene_bytes = static_cast<size_t>(W.bytes_nodes) + W.bytes_refs + W.bytes_spheres + W.bytes_quads;
     const uint32_t level = static_cast<uint32_t>(dev::kBlock * sizeof(SE));  // one stack level
-    const uint32_t nn = static_cast<uint32_t>(s->dnodes.size() - 1);      // the sentinel's index
+    // the sentinel is the last node; refs are byte offsets into the f32 node array
+    W.sentinel = static_cast<uint32_t>(s->dnodes.size() - 1) << kNodeFShift;
+    W.f32_ok = s->dev[device].f32_ok ? 1u : 0u;
+    W.tmin32 = static_cast<float>(cam->t_min);
     const bool force_global = std::getenv("CRT_NO_LDS_SCENE") != nullptr;
     // LDS stacks: [data][guard level: sentinel][levels 0..depth]; walk() may also read the level
     // below the guard, so the guard starts at least one level into the allocation
@@ -1368,26 +1652,27 @@ static int dispatch_render(const crt_scene* s, int device, const crt_camera* cam
         W.lds_spheres = W.lds_refs + W.bytes_refs;
         W.lds_quads = W.lds_spheres + W.bytes_spheres;
         W.lds_stack = stack_at(scene_bytes);
-        W.sentinel = nn * static_cast<uint32_t>(sizeof(DevNode));  // LDS byte offset
         return launch_render<SE, false, true>(s, device, cam, W, W.lds_stack + stack_bytes, d_rgb, st, count_stats);
     }
     // HBM scene: the top of the (breadth-first) node array goes to LDS as far as it fits beside
-    // the stack without costing resident blocks (5 blocks of 4 waves, the VGPR limit, at
-    // <= 32 KB each)
-    const size_t per_block = 32 * 1024;
+    // the stack without costing resident blocks (CRT_WAVES_PER_EU blocks of 4 waves, the VGPR
+    // limit); W.ntop counts bytes of f32 nodes
+    const size_t per_block = 160 * 1024 / CRT_WAVES_PER_EU;  // LDS per block at the VGPR occupancy
     const bool no_top = std::getenv("CRT_NO_LDS_TOP") != nullptr;
+    const size_t all_nodes = s->dnodes.size() * sizeof(DevNodeF);
+    auto top_bytes = [&](size_t room) {
+        return no_top ? 0u : static_cast<uint32_t>(std::min(all_nodes, room / sizeof(DevNodeF) * sizeof(DevNodeF)));
+    };
     if (stack_bytes <= kLdsStackBudget && std::getenv("CRT_FORCE_GSTACK") == nullptr) {
         const size_t room = per_block > stack_bytes + 2 * level ? per_block - stack_bytes - 2 * level : 0;
-        W.ntop = no_top ? 0 : static_cast<uint32_t>(std::min(s->dnodes.size(), room / sizeof(DevNode)));
+        W.ntop = top_bytes(room);
         W.lds_nodes = 0;
-        W.lds_stack = stack_at(align16(W.ntop * sizeof(DevNode)));
-        W.sentinel = nn;
+        W.lds_stack = stack_at(align16(W.ntop));
         return launch_render<SE, false, false>(s, device, cam, W, W.lds_stack + stack_bytes, d_rgb, st, count_stats);
     }
-    W.ntop = no_top ? 0 : static_cast<uint32_t>(std::min(s->dnodes.size(), per_block / sizeof(DevNode)));
+    W.ntop = top_bytes(per_block);
     W.lds_nodes = 0;
-    W.sentinel = nn;
-    return launch_render<SE, true, false>(s, device, cam, W, W.ntop * sizeof(DevNode), d_rgb, st, count_stats);
+    return launch_render<SE, true, false>(s, device, cam, W, W.ntop, d_rgb, st, count_stats);
 }
 
 int device_render(const crt_scene* s, int device, const crt_camera* cam, const crt_tiling* t,
@@ -1430,11 +1715,12 @@ int device_render(const crt_scene* s, int device, const crt_camera* cam, const c
     W.tiles_y = (W.owned_rows + 7) / 8;
     W.tiles = W.tiles_x * W.tiles_y;
     W.sphere_only = (s->quads.empty() && !s->spheres.empty()) ? 1u : 0u;
+    W.spheres_f32 = (W.sphere_only && s->dev[device].spheres_f32_ok) ? 1u : 0u;
     W.exact_slab = (s->exact_slab || std::getenv("CRT_EXACT_SLAB") != nullptr) ? 1u : 0u;
     hipStream_t st = static_cast<hipStream_t>(stream);
     if (count_stats) HIP_TRY(hipStreamCreate(&st));
     int r;
-    if (s->dnodes.size() < 65536)
+    if ((s->dnodes.size() << kNodeFShift) <= 65536)  // every ref fits a u16 stack entry
         r = dispatch_render<uint16_t>(s, device, cam, W, d_rgb, st, count_stats);
     else
         r = dispatch_render<uint32_t>(s, device, cam, W, d_rgb, st, count_stats);

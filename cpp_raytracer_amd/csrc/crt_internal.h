@@ -32,11 +32,41 @@ constexpr uint32_t kNodeAlways = 1u;
 // loop's only exit test is "entered a node with a primitive count" (crt_device.hip walk()).
 constexpr uint32_t kSentinelCount = 0xffffffffu;
 
+// The render kernel's walk reads a compact single-precision copy of the same node array
+// (32 bytes, two 16-byte loads) and decides most node tests in f32 with a proven error margin,
+// falling back to the f64 node above only where the margin cannot decide (crt_device.hip walk()).
+// Node references are byte offsets into this array (index * 32), in LDS and in HBM alike; an
+// interior node's right child carries the split axis in its (always zero) low five bits.
+//   interior: w0 = right_ref | axis, w1 = left_ref (< 2^31)
+//   leaf:     w0 = first primitive slot, w1 = 0x80000000 | count
+//   sentinel: w0 = its own ref | 3, w1 = 0xffffffff
+// Bounds are the f64 bounds rounded to nearest; the f32 decisions need every finite bound within
+// [-2^40, 2^40] (infinite bounds are exact), else the kernel decides every node in f64.
+struct alignas(16) DevNodeF {
+    float b[6];         // x.min x.max y.min y.max z.min z.max
+    uint32_t w0, w1;
+};
+static_assert(sizeof(DevNodeF) == 32, "f32 node is 32 bytes");
+constexpr uint32_t kNodeFShift = 5;            // ref = index << 5
+constexpr uint32_t kLeafFlagF = 0x80000000u;   // w1 of a leaf / the sentinel
+constexpr uint32_t kSentinelW1 = 0xffffffffu;
+constexpr double kF32BoundMax = 0x1p40;
+
 // Sphere (sphere.h:16-18): centre + radius in one 32-byte record.
 struct alignas(16) DevSphere {
     double c[3];
     double r;
 };
+
+// The sphere candidate filter of the render kernel's two-pass leaves (crt_device.hip
+// sphere_pair_candidates) reads spheres two at a time in packed f32: record i holds slots i and
+// i + 1 (the last record's second half is zero). r2e = RN32(r^2 (1 + 2^-14) + 2^22 |c - c32|^2)
+// folds the rounding of the centre into the radius. Needs |c_k|, |r| <= 2^30 for every sphere.
+struct alignas(16) DevSpherePair {
+    float cx[2], cy[2], cz[2], r2e[2];
+};
+static_assert(sizeof(DevSpherePair) == 32, "sphere pair record");
+constexpr double kF32SphereMax = 0x1p30;
 
 // Parallelogram (parallelogram.h:138-170) with the ctor's precomputed normals.
 struct alignas(16) DevQuad {
@@ -62,8 +92,12 @@ struct DeviceCopy {
     void* base = nullptr;
     size_t bytes = 0;
     DevNode* nodes = nullptr;
+    DevNodeF* fnodes = nullptr;   // f32 walk copy (refs = byte offsets)
+    bool f32_ok = false;          // every finite node bound within +-kF32BoundMax
     uint32_t* refs = nullptr;
     DevSphere* spheres = nullptr;
+    DevSpherePair* spair = nullptr;  // f32 filter records (slot i, i + 1)
+    bool spheres_f32_ok = false;     // every sphere within +-kF32SphereMax
     uint32_t* sphere_mat = nullptr;
     DevQuad* quads = nullptr;
     uint32_t* quad_mat = nullptr;

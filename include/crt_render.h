@@ -167,6 +167,9 @@ typedef struct crt_render_stats {
      * work = nodes_visited, sphere+parallelogram tests, rays respectively */
     uint64_t wave_iters_walk, wave_iters_leaf, wave_iters_shade;
     uint64_t ticks_tail;  /* summed per wave: ticks from its first idle lane to its end */
+    /* node tests the f32 walk could not decide (decided in f64), and the wave iterations that
+     * ran such a test */
+    uint64_t slow_node_tests, wave_iters_slow;
 } crt_render_stats;
 
 /* ---- entry points ---------------------------------------------------------------------- */

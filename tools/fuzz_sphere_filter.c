@@ -64,6 +64,53 @@ static int candidate_v7(const double c[3], double r, const double o[3], const do
     return !((-b - sqa) - m > hi || (-b + sqa) + m < lo);
 }
 
+/* The f32 filter (crt_device.hip sphere_candidate_f32 + sphere_f32 / leaf_f32 setup), operation
+ * for operation: per sphere c32 = RN32(c), r2e = RN32(r^2 (1 + 2^-14) + 2^22 |c - c32|^2); per ray
+ * o32, d32, a32 = RN32(a), kap = RN32(2^22 |o - o32|^2 + 2^-50), hi32 = RN32(tmax a (1 + 2^-20)),
+ * lo32 = RN32(tmin a (1 - 2^-20)). Returns -1 when the ray or sphere is outside the f32 range
+ * (the kernel then runs the exact test on every sphere). */
+static int f32_ray_ok(const double o[3], const double d[3], double a) {
+    for (int k = 0; k < 3; ++k)
+        if (!(fabs(o[k]) <= 0x1p30 && fabs(d[k]) <= 0x1p30)) return 0;
+    return a >= 0x1p-60 && a <= 0x1p60;
+}
+static int f32_sphere_ok(const double c[3], double r) {
+    for (int k = 0; k < 3; ++k)
+        if (!(fabs(c[k]) <= 0x1p30)) return 0;
+    return r >= 0 && r <= 0x1p30;
+}
+static int candidate_f32(const double c[3], double r, const double o[3], const double d[3], double a,
+                         double tmin, double tmax) {
+    float c32[3], o32[3], d32[3];
+    double dc2 = 0, do2 = 0;
+    for (int k = 0; k < 3; ++k) {
+        c32[k] = (float)c[k];
+        o32[k] = (float)o[k];
+        d32[k] = (float)d[k];
+        dc2 += (c[k] - (double)c32[k]) * (c[k] - (double)c32[k]);
+        do2 += (o[k] - (double)o32[k]) * (o[k] - (double)o32[k]);
+    }
+    const float r2e = (float)(r * r * (1 + 0x1p-14) + dc2 * 0x1p22);
+    const float kap = (float)(do2 * 0x1p22 + 0x1p-50);
+    const float a32 = (float)a;
+    const float hi32 = (float)(tmax * a * (1 + 0x1p-20));
+    const float lo32 = (float)(tmin * a * (1 - 0x1p-20));
+    /* per sphere */
+    const float xx = o32[0] - c32[0], xy = o32[1] - c32[1], xz = o32[2] - c32[2];
+    const float b = fmaf(d32[2], xz, fmaf(d32[1], xy, d32[0] * xx));
+    const float q = fmaf(xz, xz, fmaf(xy, xy, xx * xx));
+    const float g = fmaf(q, 1 - 0x1p-15f, -(r2e + kap));
+    const float D = fmaf(b, b, -(a32 * g));
+    const float y = -b - hi32, w = b + lo32;
+    const float z = fmaxf(y, w);
+    const float zz = z * fabsf(z);
+    return !(fmaxf(zz, 0.f) > D);
+}
+
+static long viol32 = 0, rej32 = 0, tot32 = 0;
+static int cur_fam = 0;
+static long fam_tot[6], fam_rej64[6], fam_rej32[6];
+
 static double lim_tmax(double tmax, double a) { return tmax * a * (1 + 0x1p-30); }
 static double lim_tmin(double tmin, double a) { return tmin * a * (1 - 0x1p-30); }
 
@@ -75,6 +122,20 @@ static void check(const double c[3], double r, const double o[3], const double d
     const int e = exact(c, r, o, d, tmin, tmax);
     const int f = candidate(c, r, o, d, a, lim_tmin(tmin, a), lim_tmax(tmax, a));
     const int f7 = candidate_v7(c, r, o, d, a, lim_tmin(tmin, a), lim_tmax(tmax, a));
+    if (f32_ray_ok(o, d, a) && f32_sphere_ok(c, r)) {
+        const int g = candidate_f32(c, r, o, d, a, tmin, tmax);
+        ++tot32;
+        rej32 += !g;
+        fam_tot[cur_fam]++;
+        fam_rej32[cur_fam] += !g;
+        fam_rej64[cur_fam] += !f;
+        if (e && !g) {
+            if (viol32 < 10)
+                printf("F32 VIOLATION c=(%a %a %a) r=%a o=(%a %a %a) d=(%a %a %a) tmin=%a tmax=%a\n", c[0], c[1], c[2],
+                       r, o[0], o[1], o[2], d[0], d[1], d[2], tmin, tmax);
+            ++viol32;
+        }
+    }
     rej7 += !f7;
     weaker += (!f7 && f);
     ++total;
@@ -103,6 +164,7 @@ int main(int argc, char** argv) {
     const double tmin = 0.00001;
     for (long i = 0; i < n; ++i) {
         const int fam = (int)(i % 6);
+        cur_fam = fam;
         double c[3], o[3], d[3], r, tmax;
         const double scale = pow(10.0, urange(-3, 3));
         rand_unit(d);
@@ -176,5 +238,10 @@ int main(int argc, char** argv) {
     printf("cases %ld  exact accepts %ld  filter rejects %ld (%.1f%%)  violations %ld\n", total, acc, rej,
            100.0 * rej / total, viol);
     printf("v7 filter rejects %ld; kept by this filter but rejected by v7: %ld\n", rej7, weaker);
-    return viol != 0;
+    printf("f32 filter: cases %ld  rejects %ld (%.1f%%)  violations %ld\n", tot32, rej32, 100.0 * rej32 / (tot32 ? tot32 : 1),
+           viol32);
+    for (int k = 0; k < 6; ++k)
+        printf("  family %d: %ld cases, f64 filter rejects %.1f%%, f32 filter %.1f%%\n", k, fam_tot[k],
+               100.0 * fam_rej64[k] / (fam_tot[k] ? fam_tot[k] : 1), 100.0 * fam_rej32[k] / (fam_tot[k] ? fam_tot[k] : 1));
+    return viol != 0 || viol32 != 0;
 }
