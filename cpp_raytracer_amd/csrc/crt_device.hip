@@ -69,6 +69,13 @@ struct Work {
     uint32_t row_block, tile_count, tile_index;
     uint32_t tiles_x, tiles_y, tiles;  // 8x8 pixel tiles over (owned rows x width)
     uint32_t chunks, chunk_len;        // sample chunks per pixel
+    // block -> (tile, chunk range): bulk blocks own pool_chunks chunks of a tile (chunks [0,
+    // bulk_chunks), `groups` blocks per tile), the blocks after them tail_pool_chunks (chunks
+    // [bulk_chunks, chunks), `tail_groups` blocks per tile); a block's unit pool is 64 pixels x
+    // its chunks, shared by its waves
+    uint32_t pool_chunks, groups, bulk_chunks, tail_pool_chunks, tail_groups;
+    uint32_t lds_pool;      // LDS offset of the block's pool counter
+    uint64_t bulk_blocks;
     // LDS layout of the scene-staging kernels (byte offsets / 16-byte padded sizes)
     uint32_t lds_nodes, lds_refs, lds_spheres, lds_quads, lds_stack;
     uint32_t bytes_nodes, bytes_refs, bytes_spheres, bytes_quads;
@@ -1077,14 +1084,18 @@ __device__ __forceinline__ void stage_lds(unsigned char* dst, const void* src, u
     for (uint32_t i = threadIdx.x; i < bytes / 16; i += kBlock) d[i] = s[i];
 }
 
-// The render kernel. Thread -> (sample chunk, pixel); each wave starts on one 8x8 pixel tile.
+// The render kernel. Block -> (8x8 pixel tile, a range of sample chunks): a pool of 64 x (its
+// chunks) (chunk, pixel) units that the lanes of the block's waves draw from as they finish
+// them, so the waves of a block finish together (the block's LDS and wave slots are released
+// only when all of them are done). The blocks dispatched last own fewer chunks
+// (Work::tail_pool_chunks), so the kernel drains quickly.
 // Persistent per-lane state machine (WALK -> LEAF -> ... -> DONE -> shade -> WALK) in traversal
 // rounds: every walking lane walks the DFS to its next entered leaf (or the end of its
 // traversal), then the lanes holding a leaf test it together. Lanes whose ray is finished park
 // until kShadeBatch of them are finished (or nobody traverses), then shade together, and a
 // finished path starts the lane's next sample at once (path regeneration). So the shading code
 // runs with many lanes active, and a wave is never held by its slowest ray or path.
-// Samples are summed in sample order into partial[chunk][pixel].
+// A unit's samples are summed in sample order into partial[chunk][pixel].
 // LSCENE: nodes, primitive refs, spheres and parallelograms are staged in LDS first.
 // 4 waves per SIMD (128 VGPRs): the f32 walk / packed sphere filter state does not fit 96
 // VGPRs without ~66 spills (5 waves: 3932 vs 4158 Msamples/s on config 2)
@@ -1132,22 +1143,31 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRT_WAVE
     }
     // The camera constants are read from an LDS copy in start_path / shade: held in SGPRs for
     // the whole kernel they would spill (into VGPR lanes, reloaded with v_readlane per use).
-    if (threadIdx.x == 0) *reinterpret_cast<CamView*>(smem + W.lds_cam) = C;
+    uint32_t* const pool_next = reinterpret_cast<uint32_t*>(smem + W.lds_pool);
+    if (threadIdx.x == 0) {
+        *reinterpret_cast<CamView*>(smem + W.lds_cam) = C;
+        *pool_next = 0;
+    }
     __syncthreads();
     const CamView& CL = *reinterpret_cast<const CamView*>(smem + W.lds_cam);
     const float tmin32 = W.tmin32;  // a kernel argument (SGPR): no conversion in the walk loop
     const uint32_t lane = threadIdx.x & 63;
-    const uint64_t wave = (static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x) >> 6;
-    // tile-major: the chunks of one 8x8 tile are consecutive waves, so the four waves of a block
-    // share a tile, cost about the same and release the block's slot together
-    const uint32_t chunk = static_cast<uint32_t>(wave % W.chunks);
-    const uint32_t tile = static_cast<uint32_t>(wave / W.chunks);
+    // block-uniform (SGPRs): the tile coordinates stay live for the whole kernel
+    const uint64_t block = blockIdx.x;
+    uint32_t tile, chunk0, nch;
+    if (block < W.bulk_blocks) {
+        tile = static_cast<uint32_t>(block / W.groups);
+        chunk0 = static_cast<uint32_t>(block % W.groups) * W.pool_chunks;
+        nch = W.pool_chunks;
+    } else {
+        const uint64_t b2 = block - W.bulk_blocks;
+        tile = static_cast<uint32_t>(b2 / W.tail_groups);
+        chunk0 = W.bulk_chunks + static_cast<uint32_t>(b2 % W.tail_groups) * W.tail_pool_chunks;
+        nch = W.tail_pool_chunks;
+    }
     LaneCounters ctr{};
     const unsigned long long t_start = COUNT ? wall_clock64() : 0;
     const uint32_t tx = tile % W.tiles_x, ty = tile / W.tiles_x;
-    const uint32_t col = tx * 8 + (lane & 7);
-    const uint32_t k = ty * 8 + (lane >> 3);
-    const bool valid = chunk < W.chunks && col < C.w && k < W.owned_rows;
     // stack levels 0..depth of this lane, above a guard level holding the sentinel reference
     // and one more level walk() may read (two guard levels in HBM; in LDS the level below the
     // guard is other data)
@@ -1160,23 +1180,63 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRT_WAVE
         st.stride = kBlock;
     }
     st.base[-static_cast<ptrdiff_t>(st.stride)] = static_cast<SE>(W.sentinel);
-    const uint32_t row = valid ? owned_row(W, k) : 0;
-    const uint32_t pixel = row * C.w + col;
-    uint32_t s = chunk * W.chunk_len;
-    const uint32_t s_end = valid ? min(C.spp, s + W.chunk_len) : s;
+    // The block's pool of work units: unit u = (chunk chunk0 + u / 64, pixel u % 64 of the
+    // tile), in that order. Lanes that finish a unit take the next ones (one LDS atomic per wave
+    // and draw, then in lane order), so no lane idles until the pool is dry; a unit's sum goes to
+    // partial[chunk][pixel] whichever lane traced it, so frames do not depend on the schedule.
+    const uint32_t pool = 64 * nch;
+    // the lane's unit and sample; its chunk, tile pixel and row are recomputed where needed
+    // (kept live across the phases they would spill)
+    uint32_t u = 0, s = 0;
     double acc[3] = {0, 0, 0};
     Path P;
     Trav R;
     R.state = kIdle;
-    // max_depth == 0: ray_color returns RGB::zero() for every sample (camera.h:211-213)
-    if (valid && C.max_depth > 0 && s < s_end) {
-        start_path(CL, row, col, sample_seed(C.base_seed, pixel, s), P);
-        trav_init(P.o, P.d, W.f32_ok != 0, R);
-        if (COUNT) ctr.rays++;
-    }
+    bool need = true, start = false;
     uint32_t cw = 0, cl = 0, cs = 0;  // wall_clock64 ticks (100 MHz), differences mod 2^32
     unsigned long long t_first_idle = 0;
     while (true) {
+        // lanes without a unit draw from the pool until each holds a unit with samples to trace
+        // or the pool is dry. A unit off the image or past spp has no pixel sum; one with
+        // max_depth == 0 sums RGB::zero() (camera.h:211-213) and is written at once.
+        while (true) {
+            const uint64_t m = __ballot(need);
+            if (m == 0) break;
+            const uint32_t leader = static_cast<uint32_t>(__ffsll(static_cast<long long>(m)) - 1);
+            uint32_t base = 0;
+            if (lane == leader) base = atomicAdd(pool_next, static_cast<uint32_t>(__popcll(m)));
+            base = __builtin_amdgcn_readlane(base, leader);
+            if (need) {
+                u = base + __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32),
+                                                     __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0u));
+                if (u >= pool) {
+                    need = false;
+                } else {
+                    const uint32_t chunk = chunk0 + (u >> 6);
+                    const uint32_t col = tx * 8 + (u & 7), k = ty * 8 + ((u >> 3) & 7);
+                    if (chunk < W.chunks && col < C.w && k < W.owned_rows) {
+                        s = chunk * W.chunk_len;
+                        if (C.max_depth > 0) {
+                            need = false;
+                            start = true;
+                        } else if (!COUNT) {
+                            double* dst = partial + (static_cast<size_t>(chunk) * W.owned_rows * C.w +
+                                                     static_cast<size_t>(k) * C.w + col) * 3;
+                            dst[0] = 0;
+                            dst[1] = 0;
+                            dst[2] = 0;
+                        }
+                    }
+                }
+            }
+        }
+        if (start) {
+            const uint32_t col = tx * 8 + (u & 7), row = owned_row(W, ty * 8 + ((u >> 3) & 7));
+            start_path(CL, row, col, sample_seed(C.base_seed, row * C.w + col, s), P);
+            trav_init(P.o, P.d, W.f32_ok != 0, R);
+            if (COUNT) ctr.rays++;
+            start = false;
+        }
         // traversal rounds (walk to the next entered leaf, test it) until enough lanes hold a
         // finished ray, or none is traversing
         while (true) {
@@ -1196,32 +1256,38 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRT_WAVE
         }
         const uint64_t m_done = __ballot(R.state == kDone);
         if (COUNT && t_first_idle == 0 && __ballot(R.state == kIdle) != 0) t_first_idle = wall_clock64();
-        if (m_done == 0) break;  // every lane idle: the chunk is finished
-        {
-            if (COUNT) cs -= static_cast<uint32_t>(wall_clock64());
-            if (R.state == kDone) {
-                if (COUNT && wave_leader()) ctr.it_shade++;
-                bool ended = shade(S, CL, P, R.found, R.ref, R.tmax, acc);
-                // a scattered ray with no bounce left returns RGB::zero() (camera.h:211-213)
-                if (!ended && P.depth == 0) ended = true;
-                if (ended) {
-                    if (++s >= s_end) R.state = kIdle;
-                    else start_path(CL, row, col, sample_seed(C.base_seed, pixel, s), P);
+        if (m_done == 0) break;  // every lane idle: the pool is dry
+        if (COUNT) cs -= static_cast<uint32_t>(wall_clock64());
+        if (R.state == kDone) {
+            if (COUNT && wave_leader()) ctr.it_shade++;
+            bool ended = shade(S, CL, P, R.found, R.ref, R.tmax, acc);
+            // a scattered ray with no bounce left returns RGB::zero() (camera.h:211-213)
+            if (!ended && P.depth == 0) ended = true;
+            if (!ended) {
+                trav_init(P.o, P.d, W.f32_ok != 0, R);
+                if (COUNT) ctr.rays++;
+            } else {
+                const uint32_t chunk = chunk0 + (u >> 6);
+                if (++s < min(C.spp, (chunk + 1) * W.chunk_len)) {
+                    start = true;  // the unit's next sample (started after the draw, with the drawers)
+                } else {  // the unit is done: its sum (samples in order) to partial[chunk][pixel]
+                    if (!COUNT) {
+                        const uint32_t col = tx * 8 + (u & 7), k = ty * 8 + ((u >> 3) & 7);
+                        double* dst = partial + (static_cast<size_t>(chunk) * W.owned_rows * C.w +
+                                                 static_cast<size_t>(k) * C.w + col) * 3;
+                        dst[0] = acc[0];
+                        dst[1] = acc[1];
+                        dst[2] = acc[2];
+                    }
+                    acc[0] = 0;
+                    acc[1] = 0;
+                    acc[2] = 0;
+                    need = true;
                 }
-                if (R.state != kIdle) {
-                    trav_init(P.o, P.d, W.f32_ok != 0, R);
-                    if (COUNT) ctr.rays++;
-                }
+                R.state = kIdle;
             }
-            if (COUNT) cs += static_cast<uint32_t>(wall_clock64());
         }
-    }
-    if (valid && !COUNT) {
-        const size_t owned_pixel = static_cast<size_t>(k) * C.w + col;
-        double* dst = partial + (static_cast<size_t>(chunk) * W.owned_rows * C.w + owned_pixel) * 3;
-        dst[0] = acc[0];
-        dst[1] = acc[1];
-        dst[2] = acc[2];
+        if (COUNT) cs += static_cast<uint32_t>(wall_clock64());
     }
     if (COUNT) {
         using ull = unsigned long long;
@@ -1533,21 +1599,53 @@ static int launch_render(const crt_scene* s, int device, const crt_camera* cam, 
     const DeviceCopy& c = s->dev[device];
     dev::Work W = w0;
     W.lds_cam = static_cast<uint32_t>(align16(lds));  // the camera copy after the rest
-    lds = W.lds_cam + align16(sizeof(dev::CamView));
+    W.lds_pool = static_cast<uint32_t>(W.lds_cam + align16(sizeof(dev::CamView)));
+    lds = W.lds_pool + 16;
     const uint64_t pixels = static_cast<uint64_t>(W.owned_rows) * cam->image_w;
     // Sample chunks: a function of spp ONLY, so every pixel's sum is grouped identically whatever
-    // the tiling / number of GPUs (bit-identical frames for 1..N devices). 24-sample chunks
-    // (21 per pixel at BASELINE spp, at most 64) keep waves short enough that 1/8 of a frame
-    // still spreads over ~8 rounds of resident waves (strong scaling), at 2% of the 1-GPU speed
-    // of 64-sample chunks.
+    // the tiling / number of GPUs / block pools / lane schedule (bit-identical frames for 1..N
+    // devices): 8 samples, or spp / 192 above 1536 spp. A block owns a pool of chunks of one 8x8
+    // tile (64 units per chunk, drawn by the lanes of its 4 waves as they finish one). On a whole
+    // frame, per tile one bulk block takes 8/9 of the chunks (56 of 63 at BASELINE spp), and one
+    // tail block the rest; all tail blocks are dispatched after all bulk blocks, so the kernel
+    // ends on short blocks. Measured on config 2 (Msamples/s, bulk/tail chunks): 56/7 4470, 48/15 4430,
+    // 63/0 4273, 24+24/15 4335, 12x5/3 4087; waves with private 3-chunk pools 4108.
+    // CRT_POOL_CHUNKS, CRT_TAIL_CHUNKS and CRT_TAIL_POOL_CHUNKS (environment) override the split;
+    // frames do not change.
     const uint32_t spp = cam->samples_per_pixel;
 #ifndef CRT_CHUNK_MIN
-#define CRT_CHUNK_MIN 24
+#define CRT_CHUNK_MIN 8
 #endif
-    W.chunk_len = std::max<uint32_t>(CRT_CHUNK_MIN, (spp + 63) / 64);
+    auto knob = [](const char* name, uint32_t dflt) {
+        const char* e = std::getenv(name);
+        return e ? static_cast<uint32_t>(std::max(0, std::min(4096, std::atoi(e)))) : dflt;
+    };
+    W.chunk_len = std::max<uint32_t>(CRT_CHUNK_MIN, (spp + 191) / 192);
     W.chunks = (spp + W.chunk_len - 1) / W.chunk_len;
-    const uint64_t waves = static_cast<uint64_t>(W.tiles) * W.chunks;
-    const uint64_t blocks = (waves * 64 + dev::kBlock - 1) / dev::kBlock;
+    // Default split: bpt bulk blocks per tile, bpt = 1 when the tiles fill CRT_BLOCK_ROUNDS (5)
+    // rounds of resident blocks, else as many as needed for that (a GPU's share of a multi-GPU
+    // frame). With 1 or 2 bulk blocks they take 8/9 of the chunks and one tail block the rest
+    // (config 2: 56+7 chunks on one GPU, 28+28+7 at 4 GPUs); with more, the blocks are already
+    // short and split the chunks evenly (at 8 GPUs 21+21+21; 18+18+18+9 was slower).
+    // tools/tile_timing.py, per-rank ms at N = 1/2/4/8: 107.5/55.3/30.2/16.7.
+    int cus = 0, per_cu = 0;
+    HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &per_cu, reinterpret_cast<const void*>(dev::render_kernel<SE, GSTACK, LSCENE, false>), dev::kBlock, lds));
+    const uint64_t target = static_cast<uint64_t>(knob("CRT_BLOCK_ROUNDS", 5)) * std::max(1, cus) * std::max(1, per_cu);
+    const uint32_t bpt = static_cast<uint32_t>(std::min<uint64_t>(W.chunks, (target + W.tiles - 1) / std::max<uint32_t>(1, W.tiles)));
+    const uint32_t nb = std::max<uint32_t>(1, bpt);
+    const uint32_t pool_dflt = nb <= 2 ? std::max<uint32_t>(1, (W.chunks - W.chunks / 9) / nb) : (W.chunks + nb - 1) / nb;
+    const uint32_t tail_dflt = nb <= 2 ? W.chunks - nb * pool_dflt : 0;
+    const uint32_t tail = std::min(W.chunks, knob("CRT_TAIL_CHUNKS", tail_dflt));
+    W.pool_chunks = std::max<uint32_t>(1, knob("CRT_POOL_CHUNKS", pool_dflt));
+    W.groups = (W.chunks - tail) / W.pool_chunks;
+    W.bulk_chunks = W.groups * W.pool_chunks;
+    // the tail: every chunk the bulk blocks leave, in one block per tile by default
+    W.tail_pool_chunks = std::max<uint32_t>(1, knob("CRT_TAIL_POOL_CHUNKS", W.chunks - W.bulk_chunks));
+    W.tail_groups = (W.chunks - W.bulk_chunks + W.tail_pool_chunks - 1) / W.tail_pool_chunks;
+    W.bulk_blocks = static_cast<uint64_t>(W.tiles) * W.groups;
+    const uint64_t blocks = W.bulk_blocks + static_cast<uint64_t>(W.tiles) * W.tail_groups;
     if (blocks > 0x7fffffffull) return fail(CRT_E_INVALID, "frame too large for one launch");
     const size_t plane = static_cast<size_t>(pixels) * 3;  // partials indexed by owned pixel
 
