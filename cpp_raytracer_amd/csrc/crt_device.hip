@@ -612,20 +612,35 @@ __device__ __forceinline__ bool finite_nonzero(double x) { return fabs(x) < __bu
 __device__ __forceinline__ bool finite(double x) { return fabs(x) < __builtin_inf(); }
 __device__ __forceinline__ float tmax_f32(double t) { return static_cast<float>(fmin(t, 0x1p100)); }
 
+// 1/x within 2^-51 relative for 2^-1000 <= |x| <= 2^1000: v_rcp_f64 and two Newton steps (the
+// first steps of hipcc's own f64 division, without its scaling and final correction). The walk's
+// f32 node test only needs RN32(1/d) and RN32(o/d) within its error analysis, which has room for
+// it (walk()); the f64 decisions (slab64, the EXACT walk) divide exactly.
+__device__ __forceinline__ double recip_nr(double x) {
+    double r = __builtin_amdgcn_rcp(x);
+    r = fma(r, fma(-x, r, 1.0), r);
+    return fma(r, fma(-x, r, 1.0), r);
+}
+__device__ __forceinline__ bool dir_ok(double x) { return fabs(x) >= 0x1p-1000 && fabs(x) <= 0x1p1000; }
+
 // f32_ok: the scene's node bounds fit the f32 error analysis (Work::f32_ok)
 __device__ __forceinline__ void trav_init(const double o[3], const double d[3], bool f32_ok, Trav& R) {
-    const double inv[3] = {1 / d[0], 1 / d[1], 1 / d[2]};
+    const double inv[3] = {recip_nr(d[0]), recip_nr(d[1]), recip_nr(d[2])};
     R.a = d[0] * d[0] + d[1] * d[1] + d[2] * d[2];
     R.tmax = __builtin_inf();
     R.tmax32 = 0x1p100f;
     R.cur = 0;
     R.sp = 0;
     R.ref = 0;
-    const bool fast = finite_nonzero(inv[0]) && finite_nonzero(inv[1]) && finite_nonzero(inv[2]) &&
+    // NaN-free slab values (the min/max and f32 walks): 1/d finite and non-zero, o finite. Rays
+    // with a direction component outside [2^-1000, 2^1000] (zero, tiny, huge, NaN) take the EXACT
+    // walk, which is the reference's select sequence for any ray.
+    const bool fast = dir_ok(d[0]) && dir_ok(d[1]) && dir_ok(d[2]) &&
                       finite(o[0]) && finite(o[1]) && finite(o[2]);
     R.neg = (d[0] < 0 ? 1u : 0u) | (d[1] < 0 ? 2u : 0u) | (d[2] < 0 ? 4u : 0u) | (fast ? 0u : kZeroDir);
     // the f32 node test's error analysis (walk()) holds for 2^-40 <= |1/d_k| <= 2^40 and
-    // |o_k| <= 2^40; other rays get marg = inf, i.e. every node test decided in f64
+    // |o_k| <= 2^40, here ensured by 2^-39 <= |d_k| <= 2^39; other rays get marg = inf, i.e.
+    // every node test decided in f64
     bool f32 = f32_ok;
     double A = 0;
 #pragma unroll
@@ -634,7 +649,7 @@ __device__ __forceinline__ void trav_init(const double o[3], const double d[3], 
         R.inv32[k] = static_cast<float>(inv[k]);
         R.oinv32[k] = static_cast<float>(oi);
         A = fmax(A, fabs(oi));
-        f32 = f32 && fabs(inv[k]) <= 0x1p40 && fabs(inv[k]) >= 0x1p-40 && fabs(o[k]) <= 0x1p40;
+        f32 = f32 && fabs(d[k]) <= 0x1p39 && fabs(d[k]) >= 0x1p-39 && fabs(o[k]) <= 0x1p40;
     }
     R.marg = f32 ? static_cast<float>(fmax(A * 0x1p-19, 0x1p-60)) : __builtin_inff();
     R.state = kWalk;
@@ -658,8 +673,9 @@ __device__ __forceinline__ void trav_init(const double o[3], const double d[3], 
 // take the EXACT variant: the reference's select sequence verbatim on the f64 node.
 //
 // The other rays decide the test in f32 first (Trav::inv32 / oinv32 / marg, DevNodeF):
-//   t'_jk = fma(b32_jk, inv32_k, -oinv32_k),  b32 = RN32(b), inv32 = RN32(inv), oinv32 =
-//   RN32(RN(o * inv)). With u = 2^-24 and A = max_k |o_k inv_k|, and |b| <= |b - o| + |o|,
+//   t'_jk = fma(b32_jk, inv32_k, -oinv32_k),  b32 = RN32(b), inv32 = RN32(inv~), oinv32 =
+//   RN32(RN(o * inv~)), inv~ = recip_nr(d) within 2^-51 of the f64 inv (its extra error, below
+//   2^-27 u (|b| + |o|) |inv|, is inside the 0.01 u of slack below). With u = 2^-24 and A = max_k |o_k inv_k|, and |b| <= |b - o| + |o|,
 //   |t' - t| <= 3.01 u (|b| + |o|) |inv| + 2.01 u64 |t| <= 2^-22.4 |t'| + 2^-21.4 A + 2^-85
 // (2^-85: f32 underflow at |inv| <= 2^40). min / max are 1-Lipschitz, so lo' = max(near', tmin')
 // and hi' = min(far', tmax') are within that bound of lo = max(near, tmin), hi = min(far, tmax)
@@ -1143,15 +1159,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRT_WAVE
     }
     // The camera constants are read from an LDS copy in start_path / shade: held in SGPRs for
     // the whole kernel they would spill (into VGPR lanes, reloaded with v_readlane per use).
-    uint32_t* const pool_next = reinterpret_cast<uint32_t*>(smem + W.lds_pool);
-    if (threadIdx.x == 0) {
-        *reinterpret_cast<CamView*>(smem + W.lds_cam) = C;
-        *pool_next = 0;
-    }
-    __syncthreads();
-    const CamView& CL = *reinterpret_cast<const CamView*>(smem + W.lds_cam);
-    const float tmin32 = W.tmin32;  // a kernel argument (SGPR): no conversion in the walk loop
-    const uint32_t lane = threadIdx.x & 63;
     // block-uniform (SGPRs): the tile coordinates stay live for the whole kernel
     const uint64_t block = blockIdx.x;
     uint32_t tile, chunk0, nch;
@@ -1165,9 +1172,21 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRT_WAVE
         chunk0 = W.bulk_chunks + static_cast<uint32_t>(b2 % W.tail_groups) * W.tail_pool_chunks;
         nch = W.tail_pool_chunks;
     }
+    const uint32_t tx = tile % W.tiles_x, ty = tile / W.tiles_x;
+    // LDS: the pool counter, then the image rows of the tile's 8 owned rows (owned_row divides)
+    uint32_t* const pool_next = reinterpret_cast<uint32_t*>(smem + W.lds_pool);
+    uint32_t* const tile_rows = pool_next + 4;
+    if (threadIdx.x == 0) {
+        *reinterpret_cast<CamView*>(smem + W.lds_cam) = C;
+        *pool_next = 0;
+    }
+    if (threadIdx.x < 8) tile_rows[threadIdx.x] = owned_row(W, ty * 8 + threadIdx.x);
+    __syncthreads();
+    const CamView& CL = *reinterpret_cast<const CamView*>(smem + W.lds_cam);
+    const float tmin32 = W.tmin32;  // a kernel argument (SGPR): no conversion in the walk loop
+    const uint32_t lane = threadIdx.x & 63;
     LaneCounters ctr{};
     const unsigned long long t_start = COUNT ? wall_clock64() : 0;
-    const uint32_t tx = tile % W.tiles_x, ty = tile / W.tiles_x;
     // stack levels 0..depth of this lane, above a guard level holding the sentinel reference
     // and one more level walk() may read (two guard levels in HBM; in LDS the level below the
     // guard is other data)
@@ -1192,7 +1211,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRT_WAVE
     Path P;
     Trav R;
     R.state = kIdle;
-    bool need = true, start = false;
+    bool need = true, start = false, cont = false;
     uint32_t cw = 0, cl = 0, cs = 0;  // wall_clock64 ticks (100 MHz), differences mod 2^32
     unsigned long long t_first_idle = 0;
     while (true) {
@@ -1231,12 +1250,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRT_WAVE
             }
         }
         if (start) {
-            const uint32_t col = tx * 8 + (u & 7), row = owned_row(W, ty * 8 + ((u >> 3) & 7));
+            const uint32_t col = tx * 8 + (u & 7), row = tile_rows[(u >> 3) & 7];
             start_path(CL, row, col, sample_seed(C.base_seed, row * C.w + col, s), P);
+        }
+        // one traversal set-up for new samples and scattered rays alike (the wave runs it once)
+        if (start || cont) {
             trav_init(P.o, P.d, W.f32_ok != 0, R);
             if (COUNT) ctr.rays++;
-            start = false;
         }
+        start = false;
+        cont = false;
         // traversal rounds (walk to the next entered leaf, test it) until enough lanes hold a
         // finished ray, or none is traversing
         while (true) {
@@ -1264,8 +1287,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRT_WAVE
             // a scattered ray with no bounce left returns RGB::zero() (camera.h:211-213)
             if (!ended && P.depth == 0) ended = true;
             if (!ended) {
-                trav_init(P.o, P.d, W.f32_ok != 0, R);
-                if (COUNT) ctr.rays++;
+                cont = true;  // the scattered ray: traversal set-up with the new samples' (above)
             } else {
                 const uint32_t chunk = chunk0 + (u >> 6);
                 if (++s < min(C.spp, (chunk + 1) * W.chunk_len)) {
@@ -1600,7 +1622,7 @@ static int launch_render(const crt_scene* s, int device, const crt_camera* cam, 
     dev::Work W = w0;
     W.lds_cam = static_cast<uint32_t>(align16(lds));  // the camera copy after the rest
     W.lds_pool = static_cast<uint32_t>(W.lds_cam + align16(sizeof(dev::CamView)));
-    lds = W.lds_pool + 16;
+    lds = W.lds_pool + 48;  // pool counter (16 B) + the tile's 8 image rows
     const uint64_t pixels = static_cast<uint64_t>(W.owned_rows) * cam->image_w;
     // Sample chunks: a function of spp ONLY, so every pixel's sum is grouped identically whatever
     // the tiling / number of GPUs / block pools / lane schedule (bit-identical frames for 1..N
