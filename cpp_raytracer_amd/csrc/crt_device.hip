@@ -1119,9 +1119,18 @@ __device__ __forceinline__ void stage_lds(unsigned char* dst, const void* src, u
 #define CRT_WAVES_PER_EU 4
 #endif
 #ifndef CRT_SHADE_BATCH
-#define CRT_SHADE_BATCH 32
+#define CRT_SHADE_BATCH 48
 #endif
 constexpr int kShadeBatch = CRT_SHADE_BATCH;
+// ...or once at least kShadeMin are and no more than kPendingMax lanes still traverse (off by
+// default: 56/32/8, 64/40/8 and 56/24/4 all measured slower than 48 alone)
+#ifndef CRT_SHADE_MIN
+#define CRT_SHADE_MIN 64
+#endif
+#ifndef CRT_PENDING_MAX
+#define CRT_PENDING_MAX 0
+#endif
+constexpr int kShadeMin = CRT_SHADE_MIN, kPendingMax = CRT_PENDING_MAX;
 
 #ifndef CRT_TOP_TREELET
 #define CRT_TOP_TREELET 1
@@ -1275,7 +1284,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRT_WAVE
             if (COUNT) cl += static_cast<uint32_t>(wall_clock64());
             const uint64_t pending = __ballot(R.state == kWalk);
             const uint64_t finished = __ballot(R.state == kDone);
-            if (pending == 0 || __popcll(finished) >= kShadeBatch) break;
+            const int nfin = __popcll(finished);
+            if (pending == 0 || nfin >= kShadeBatch || (__popcll(pending) <= kPendingMax && nfin >= kShadeMin)) break;
         }
         const uint64_t m_done = __ballot(R.state == kDone);
         if (COUNT && t_first_idle == 0 && __ballot(R.state == kIdle) != 0) t_first_idle = wall_clock64();
