@@ -5,7 +5,8 @@ One step = one whole frame of BASELINE config 2 (rtweekend_final_image scene at 
 1200x800, 500 spp, max_depth 50) rendered by the gfx950 kernel from a scene already resident in
 HBM. With N ranks (torchrun, one process per GPU) the frame's rows are dealt to ranks in 4-row
 blocks, each rank renders its blocks, and the tiles are all-gathered over RCCL (xGMI) into a full
-frame on every rank: the total work is fixed, so scaling is "strong".
+frame on every rank: the total work is fixed, so scaling is "strong". The gather of frame i runs
+on a side stream while frame i + 1 renders (double-buffered frames).
 
 Prints ONE JSON line on rank 0 (see the repo contract), with
   roofline:     algorithmic bytes of the render kernel (56 B per BVH node visited,
@@ -137,21 +138,37 @@ def main():
     log(f"scene {args.scene}: {info.num_primitives} prims, {info.num_nodes} nodes, depth {info.depth}, "
         f"BVH build {info.build_ms:.1f} ms, setup {time.time() - t0:.1f} s")
 
-    frame = torch.zeros(h, w, 3, dtype=torch.float64, device="cuda")
+    frames = [torch.zeros(h, w, 3, dtype=torch.float64, device="cuda") for _ in range(2 if distributed else 1)]
     gather = TileGather(h, w, world, rank, "cuda", row_block=rb)
     stream = torch.cuda.current_stream()
+    side = torch.cuda.Stream() if distributed else None
+    gathered = [None] * len(frames)  # per frame buffer: event after its last gather
 
-    def step(ev=None):
+    def step(i, ev=None):
+        # N > 1: frame i's tiles are all-gathered (RCCL over xGMI) on a side stream while frame
+        # i + 1 renders into the other buffer; a buffer is rendered into again only after its
+        # previous gather is done. Every frame is rendered AND assembled inside the timed region.
+        k = i % len(frames)
+        buf = frames[k]
+        if gathered[k] is not None:
+            stream.wait_event(gathered[k])
         if ev is not None:
             ev[0].record(stream)
-        scene.render_async(local, cam, frame.data_ptr(), stream.cuda_stream, tiling)
+        scene.render_async(local, cam, buf.data_ptr(), stream.cuda_stream, tiling)
         if ev is not None:
             ev[1].record(stream)
-        if distributed:  # assemble the frame from every rank's row tiles (RCCL over xGMI)
-            gather.gather(frame)
+        if distributed:
+            rendered = torch.cuda.Event()
+            rendered.record(stream)
+            with torch.cuda.stream(side):
+                side.wait_event(rendered)
+                gather.gather(buf)
+                done = torch.cuda.Event()
+                done.record(side)
+            gathered[k] = done
 
-    for _ in range(args.warmup):
-        step()
+    for i in range(args.warmup):
+        step(i)
     torch.cuda.synchronize()
     if distributed:
         dist.barrier()
@@ -159,7 +176,7 @@ def main():
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     t_start = time.perf_counter()
     for i in range(args.steps):
-        step(evs[i])
+        step(args.warmup + i, evs[i])
     torch.cuda.synchronize()
     if distributed:
         dist.barrier()
@@ -214,7 +231,7 @@ def main():
                                    f"{args.scene} seed {args.seed}, {w}x{h}, {args.spp} spp, max_depth {args.depth}",
                        "samples_per_step": h * w * args.spp, "primitives": int(info.num_primitives),
                        "bvh_nodes": int(info.num_nodes), "partition": f"{rb}-row blocks over {world} ranks, "
-                       "RCCL all-gather of tiles" if distributed else "whole frame on one GPU"},
+                       "RCCL all-gather of tiles overlapped with the next frame" if distributed else "whole frame on one GPU"},
             "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved_gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "kernel_ms": round(kernel_ms, 3),

@@ -76,6 +76,7 @@ struct Work {
     uint32_t pool_chunks, groups, bulk_chunks, tail_pool_chunks, tail_groups;
     uint32_t lds_pool;      // LDS offset of the block's pool counter
     uint64_t bulk_blocks;
+    uint32_t tile_order, tile_stride;  // dispatch order of tiles: 0 row-major, 1 reversed, 2 strided
     // LDS layout of the scene-staging kernels (byte offsets / 16-byte padded sizes)
     uint32_t lds_nodes, lds_refs, lds_spheres, lds_quads, lds_stack;
     uint32_t bytes_nodes, bytes_refs, bytes_spheres, bytes_quads;
@@ -1181,6 +1182,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRT_WAVE
         chunk0 = W.bulk_chunks + static_cast<uint32_t>(b2 % W.tail_groups) * W.tail_pool_chunks;
         nch = W.tail_pool_chunks;
     }
+    if (W.tile_order == 1) tile = W.tiles - 1 - tile;
+    else if (W.tile_order == 2) tile = static_cast<uint32_t>((static_cast<uint64_t>(tile) * W.tile_stride) % W.tiles);
     const uint32_t tx = tile % W.tiles_x, ty = tile / W.tiles_x;
     // LDS: the pool counter, then the image rows of the tile's 8 owned rows (owned_row divides)
     uint32_t* const pool_next = reinterpret_cast<uint32_t*>(smem + W.lds_pool);
@@ -1677,6 +1680,9 @@ static int launch_render(const crt_scene* s, int device, const crt_camera* cam, 
     W.tail_pool_chunks = std::max<uint32_t>(1, knob("CRT_TAIL_POOL_CHUNKS", W.chunks - W.bulk_chunks));
     W.tail_groups = (W.chunks - W.bulk_chunks + W.tail_pool_chunks - 1) / W.tail_pool_chunks;
     W.bulk_blocks = static_cast<uint64_t>(W.tiles) * W.groups;
+    W.tile_order = knob("CRT_TILE_ORDER", 0);
+    W.tile_stride = 7919;  // prime: tile * stride mod tiles is a permutation unless 7919 | tiles
+    if (W.tile_order == 2 && W.tiles % W.tile_stride == 0) W.tile_order = 0;
     const uint64_t blocks = W.bulk_blocks + static_cast<uint64_t>(W.tiles) * W.tail_groups;
     if (blocks > 0x7fffffffull) return fail(CRT_E_INVALID, "frame too large for one launch");
     const size_t plane = static_cast<size_t>(pixels) * 3;  // partials indexed by owned pixel
