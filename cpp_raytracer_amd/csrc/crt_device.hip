@@ -843,12 +843,14 @@ __device__ __forceinline__ void walk(const SceneView& S, Stack<SE>& st, const do
                 }
             }
             const bool inner = enter & (w1 < kLeafFlagF);
-            // v_bfe_u32 takes the offset from w0's low five bits: the split axis
-            const bool far_first = __builtin_amdgcn_ubfe(R.neg, w0, 1) != 0;
-            const uint32_t right = w0 & ~((1u << kNodeFShift) - 1);
-            tp[stride] = static_cast<SE>(far_first ? w1 : right);
+            // siblings are side by side, the left one 64-byte aligned: near = left | 32 when the
+            // right child comes first (v_bfe_u32 takes the offset from w0's low five bits: the
+            // split axis), far = near ^ 32. At a leaf the store lands above the live stack; at the
+            // sentinel it overwrites the guard level, which every traversal start rewrites.
+            const uint32_t near = w1 | (__builtin_amdgcn_ubfe(R.neg, w0, 1) << kNodeFShift);
+            tp[stride] = static_cast<SE>(near ^ (1u << kNodeFShift));
             stop = enter ^ inner;  // entered, not interior: a leaf or the sentinel
-            cur = inner ? (far_first ? right : w1) : top;
+            cur = inner ? near : top;
             tp += inner ? stride : -stride;
         } while (!stop);
     }
@@ -1265,8 +1267,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRT_WAVE
             const uint32_t col = tx * 8 + (u & 7), row = tile_rows[(u >> 3) & 7];
             start_path(CL, row, col, sample_seed(C.base_seed, row * C.w + col, s), P);
         }
-        // one traversal set-up for new samples and scattered rays alike (the wave runs it once)
+        // one traversal set-up for new samples and scattered rays alike (the wave runs it once);
+        // the guard level below the stack gets the sentinel back (the f32 walk's store at the
+        // sentinel overwrote it)
         if (start || cont) {
+            st.base[-static_cast<ptrdiff_t>(st.stride)] = static_cast<SE>(W.sentinel);
             trav_init(P.o, P.d, W.f32_ok != 0, R);
             if (COUNT) ctr.rays++;
         }
@@ -1497,9 +1502,15 @@ int device_upload(crt_scene* s, int device) {
             f.b[k] = static_cast<float>(n.b[k]);  // round to nearest
             if (!std::isinf(n.b[k]) && !(std::fabs(n.b[k]) <= kF32BoundMax)) f32_ok = false;
         }
-        if (n.count == 0) {
-            f.w0 = (n.index << kNodeFShift) | n.axis;
+        if (n.count == 0 && n.index == n.flags + 1 && !(n.flags & 1u)) {
+            // interior: children side by side, the left one at an even index (stage()); the walk
+            // takes the right child as left | 32
+            f.w0 = n.axis;
             f.w1 = n.flags << kNodeFShift;
+        } else if (n.count == 0) {
+            // the root of an empty tree (empty box, no children): an empty leaf
+            f.w0 = 0;
+            f.w1 = kLeafFlagF;
         } else if (n.count == kSentinelCount) {
             // "axis" 3: R.neg bit 3 (kZeroDir) is clear in the f32 walk, so the far child the
             // walk stores at the sentinel (into the guard level) is w0 & ~31, the sentinel itself

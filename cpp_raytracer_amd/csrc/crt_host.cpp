@@ -470,22 +470,38 @@ static void stage(crt_scene* s) {
             todo.push_back(l);
         }
     }
-    for (size_t k = 0; k < bfs.size(); ++k) pos[bfs[k]] = static_cast<uint32_t>(k);
-    s->dnodes.resize(nn + 1);
+    // Device position of bfs[k]: the root at 0, an unused pad node at 1, bfs[k] at k + 1 for
+    // k >= 1, so that every sibling pair (pushed together above) starts at an even position: a
+    // right child is its left sibling + 1 and the pair fills one aligned 64-byte line of f32
+    // nodes (the render walk derives both children from the left one).
+    auto place = [](size_t k) { return static_cast<uint32_t>(k == 0 ? 0 : k + 1); };
+    for (size_t k = 0; k < bfs.size(); ++k) pos[bfs[k]] = place(k);
+    const size_t nd = nn ? nn + 1 : 0;  // tree + pad
+    s->dnodes.resize(nd + 1);
     s->exact_slab = false;
     {  // the sentinel (kSentinelCount) after the tree's nodes
-        DevNode& z = s->dnodes[nn];
+        DevNode& z = s->dnodes[nd];
         for (int k = 0; k < 3; ++k) {
             z.b[2 * k] = -std::numeric_limits<double>::infinity();
             z.b[2 * k + 1] = std::numeric_limits<double>::infinity();
         }
-        z.index = z.flags = static_cast<uint32_t>(nn);
+        z.index = z.flags = static_cast<uint32_t>(nd);
         z.count = kSentinelCount;
+        z.axis = 0;
+    }
+    if (nn) {  // the pad: an empty one-primitive leaf no node refers to
+        DevNode& z = s->dnodes[1];
+        for (int k = 0; k < 3; ++k) {
+            z.b[2 * k] = std::numeric_limits<double>::infinity();
+            z.b[2 * k + 1] = -std::numeric_limits<double>::infinity();
+        }
+        z.index = z.flags = 0;
+        z.count = 1;
         z.axis = 0;
     }
     for (size_t q = 0; q < bfs.size(); ++q) {
         const crt_bvh_node& n = s->nodes[bfs[q]];
-        DevNode& d = s->dnodes[q];
+        DevNode& d = s->dnodes[place(q)];
         for (int k = 0; k < 3; ++k)
             if (!(n.bounds[2 * k] <= n.bounds[2 * k + 1]) && !(n.flags & kNodeAlways)) s->exact_slab = true;
         std::memcpy(d.b, n.bounds, sizeof d.b);
