@@ -771,7 +771,11 @@ __device__ __forceinline__ void walk(const SceneView& S, Stack<SE>& st, const do
     uint32_t w0, w1;  // the last node's DevNodeF words (leaf / sentinel at the exit)
     bool stop;
     if (EXACT) {
-        const double inv[3] = {1 / d[0], 1 / d[1], 1 / d[2]};
+        // divided here: without the barrier the compiler hoists these three divisions out of
+        // the traversal rounds into every shade round, although the EXACT walk is rare
+        double dx = d[0], dy = d[1], dz = d[2];
+        asm volatile("" : "+v"(dx), "+v"(dy), "+v"(dz));
+        const double inv[3] = {1 / dx, 1 / dy, 1 / dz};
         do {
             NodeLines nd;
             node_lines(node64(S, cur), nd);
