@@ -248,6 +248,9 @@ def main():
                 "walk": round(cnt.nodes_visited / max(1, 64 * cnt.wave_iters_walk), 4),
                 "leaf": round((cnt.sphere_tests + cnt.parallelogram_tests) / max(1, 64 * cnt.wave_iters_leaf), 4),
                 "shade": round(cnt.rays / max(1, 64 * cnt.wave_iters_shade), 4)},
+            "two_pass_leaves": {"candidates_per_ray": round(cnt.candidate_tests / max(1, cnt.rays), 4),
+                                "candidate_lane_utilization": round(cnt.candidate_tests / max(1, 64 * cnt.wave_iters_candidates), 4),
+                                "candidate_wave_iters_per_filter_wave_iter": round(cnt.wave_iters_candidates / max(1, cnt.wave_iters_leaf), 4)},
             "f32_walk": {"f64_decided_node_tests": round(cnt.slow_node_tests / max(1, cnt.nodes_visited), 6),
                          "walk_iters_with_f64": round(cnt.wave_iters_slow / max(1, cnt.wave_iters_walk), 6)},
             "cpu_baseline": cpu,

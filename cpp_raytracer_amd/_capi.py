@@ -83,7 +83,8 @@ class RenderStats(C.Structure):
                 ("ticks_shade", C.c_uint64), ("ticks_total", C.c_uint64),
                 ("wave_iters_walk", C.c_uint64), ("wave_iters_leaf", C.c_uint64),
                 ("wave_iters_shade", C.c_uint64), ("ticks_tail", C.c_uint64),
-                ("slow_node_tests", C.c_uint64), ("wave_iters_slow", C.c_uint64)]
+                ("slow_node_tests", C.c_uint64), ("wave_iters_slow", C.c_uint64),
+                ("candidate_tests", C.c_uint64), ("wave_iters_candidates", C.c_uint64)]
 
 
 # numpy views of the same records (for bulk scene I/O)

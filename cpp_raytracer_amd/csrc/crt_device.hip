@@ -96,6 +96,7 @@ struct Counters {
     unsigned long long cyc_tail;  // from the wave's first idle lane (chunk done) to its end
     unsigned long long it_walk, it_leaf, it_shade;  // wave iterations (lane utilization)
     unsigned long long slow_nodes, it_slow;  // node tests decided in f64 (lanes / wave iterations)
+    unsigned long long cand, it_cand;        // two-pass leaves: exact tests of candidates (lanes / wave iterations)
 };
 
 // one lane's counts in the instrumented pass (32-bit: a lane handles one sample chunk), added to
@@ -104,6 +105,7 @@ struct LaneCounters {
     uint32_t rays, nodes, sphere_tests, quad_tests;
     uint32_t it_walk, it_leaf, it_shade;
     uint32_t slow_nodes, it_slow;
+    uint32_t cand, it_cand;
 };
 
 // counts one per wave: only the lowest active lane increments
@@ -902,6 +904,10 @@ __device__ __forceinline__ void leaf_step(const SceneView& S, Stack<SE>& st, con
         }
         cand &= ~(range.y & 1u);  // an odd count's last verdict is the slot after the leaf
         while (cand) {
+            if (COUNT) {
+                ctr.cand++;
+                if (wave_leader()) ctr.it_cand++;
+            }
             const uint32_t b = 31 - __builtin_clz(cand);
             cand ^= 1u << b;
             const uint32_t i = range.x + (nbits - 1 - b);
@@ -1353,6 +1359,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRT_WAVE
         atomicAdd(&counters->it_shade, static_cast<ull>(ctr.it_shade));
         atomicAdd(&counters->slow_nodes, static_cast<ull>(ctr.slow_nodes));
         atomicAdd(&counters->it_slow, static_cast<ull>(ctr.it_slow));
+        atomicAdd(&counters->cand, static_cast<ull>(ctr.cand));
+        atomicAdd(&counters->it_cand, static_cast<ull>(ctr.it_cand));
     }
 }
 
@@ -1641,7 +1649,7 @@ static size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
 #define CRT_LDS_BUDGET_KB 40
 #endif
 constexpr size_t kLdsSceneBudget = CRT_LDS_BUDGET_KB * 1024;  // scene + stack per block
-constexpr size_t kLdsStackBudget = 32 * 1024 * (dev::kBlock / 256);
+constexpr size_t kLdsStackBudget = 32 * 1024 * dev::kBlock / 256;
 
 template <typename SE, bool GSTACK, bool LSCENE>
 static int launch_render(const crt_scene* s, int device, const crt_camera* cam, const dev::Work& w0,
@@ -1766,6 +1774,8 @@ static int launch_render(const crt_scene* s, int device, const crt_camera* cam, 
         count_stats->ticks_tail = h.cyc_tail;
         count_stats->slow_node_tests = h.slow_nodes;
         count_stats->wave_iters_slow = h.it_slow;
+        count_stats->candidate_tests = h.cand;
+        count_stats->wave_iters_candidates = h.it_cand;
         if (std::getenv("CRT_DEBUG_COUNTERS"))
             std::fprintf(stderr, "crt counters: rays %llu nodes %llu sphere_tests %llu quad_tests %llu it_walk %llu "
                          "it_leaf %llu it_shade %llu\n", h.rays, h.nodes, h.sphere_tests, h.quad_tests, h.it_walk,

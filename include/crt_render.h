@@ -170,6 +170,9 @@ typedef struct crt_render_stats {
     /* node tests the f32 walk could not decide (decided in f64), and the wave iterations that
      * ran such a test */
     uint64_t slow_node_tests, wave_iters_slow;
+    /* two-pass sphere leaves: exact tests of the filter's candidates, and the wave iterations
+     * of that pass (sphere_tests counts the filter's tests) */
+    uint64_t candidate_tests, wave_iters_candidates;
 } crt_render_stats;
 
 /* ---- entry points ---------------------------------------------------------------------- */
