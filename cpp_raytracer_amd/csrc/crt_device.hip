@@ -1131,6 +1131,11 @@ __device__ __forceinline__ void stage_lds(unsigned char* dst, const void* src, u
 #ifndef CRT_WAVES_PER_EU
 #define CRT_WAVES_PER_EU 4
 #endif
+// LDS-scene kernels: 5 waves per SIMD (96 VGPRs, ~55 spilled) measured +0.7% on config 2 and
+// +1.2% on config 3; the HBM-scene kernels lose 14% with it (config 4) and keep 4
+#ifndef CRT_WAVES_PER_EU_LDS
+#define CRT_WAVES_PER_EU_LDS 5
+#endif
 #ifndef CRT_SHADE_BATCH
 #define CRT_SHADE_BATCH 48
 #endif
@@ -1151,7 +1156,7 @@ constexpr int kShadeMin = CRT_SHADE_MIN, kPendingMax = CRT_PENDING_MAX;
 constexpr bool kTopTreelet = CRT_TOP_TREELET != 0;
 
 template <typename SE, bool GSTACK, bool LSCENE, bool COUNT>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRT_WAVES_PER_EU, 8))) void render_kernel(
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LSCENE ? CRT_WAVES_PER_EU_LDS : CRT_WAVES_PER_EU, 8))) void render_kernel(
     SceneView Sg, CamView C, Work W, double* __restrict__ partial, SE* __restrict__ gstack,
     Counters* __restrict__ counters) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1680,17 +1685,18 @@ static int launch_render(const crt_scene* s, int device, const crt_camera* cam, 
     };
     W.chunk_len = std::max<uint32_t>(CRT_CHUNK_MIN, (spp + 191) / 192);
     W.chunks = (spp + W.chunk_len - 1) / W.chunk_len;
-    // Default split: bpt bulk blocks per tile, bpt = 1 when the tiles fill CRT_BLOCK_ROUNDS (5)
+    // Default split: bpt bulk blocks per tile, bpt = 1 when the tiles fill CRT_BLOCK_ROUNDS (4)
     // rounds of resident blocks, else as many as needed for that (a GPU's share of a multi-GPU
     // frame). With 1 or 2 bulk blocks they take 8/9 of the chunks and one tail block the rest
     // (config 2: 56+7 chunks on one GPU, 28+28+7 at 4 GPUs); with more, the blocks are already
     // short and split the chunks evenly (at 8 GPUs 21+21+21; 18+18+18+9 was slower).
-    // tools/tile_timing.py, per-rank ms at N = 1/2/4/8: 107.5/55.3/30.2/16.7.
+    // Four rounds at 5 blocks/CU (the LDS-scene kernels) are ~5000 blocks, as five were at 4.
+    // tools/tile_timing.py, per-rank ms at N = 1/2/4/8: 91.9/49.5/27.1/16.0.
     int cus = 0, per_cu = 0;
     HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
     HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(
         &per_cu, reinterpret_cast<const void*>(dev::render_kernel<SE, GSTACK, LSCENE, false>), dev::kBlock, lds));
-    const uint64_t target = static_cast<uint64_t>(knob("CRT_BLOCK_ROUNDS", 5)) * std::max(1, cus) * std::max(1, per_cu);
+    const uint64_t target = static_cast<uint64_t>(knob("CRT_BLOCK_ROUNDS", 4)) * std::max(1, cus) * std::max(1, per_cu);
     const uint32_t bpt = static_cast<uint32_t>(std::min<uint64_t>(W.chunks, (target + W.tiles - 1) / std::max<uint32_t>(1, W.tiles)));
     const uint32_t nb = std::max<uint32_t>(1, bpt);
     const uint32_t pool_dflt = nb <= 2 ? std::max<uint32_t>(1, (W.chunks - W.chunks / 9) / nb) : (W.chunks + nb - 1) / nb;
