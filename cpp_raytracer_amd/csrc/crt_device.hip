@@ -69,14 +69,13 @@ struct Work {
     uint32_t row_block, tile_count, tile_index;
     uint32_t tiles_x, tiles_y, tiles;  // 8x8 pixel tiles over (owned rows x width)
     uint32_t chunks, chunk_len;        // sample chunks per pixel
-    // block -> (tile, chunk range): bulk blocks own pool_chunks chunks of a tile (chunks [0,
-    // bulk_chunks), `groups` blocks per tile), the blocks after them tail_pool_chunks (chunks
-    // [bulk_chunks, chunks), `tail_groups` blocks per tile); a block's unit pool is 64 pixels x
-    // its chunks, shared by its waves
-    uint32_t pool_chunks, groups, bulk_chunks, tail_pool_chunks, tail_groups;
-    uint32_t lds_pool;      // LDS offset of the block's pool counter
-    uint64_t bulk_blocks;
-    uint32_t tile_order, tile_stride;  // dispatch order of tiles: 0 row-major, 1 reversed, 2 strided
+    // work queue, taken in order by the waves of a persistent grid (render_kernel): bulk items
+    // (tile i / groups, chunks [(i % groups) * item_chunks, + item_chunks)), then tail items
+    // (tile j / tail_chunks, chunk bulk_chunks + j % tail_chunks); 64 units per chunk
+    uint32_t* queue;        // the next item (zeroed before the launch)
+    uint32_t n_items, bulk_items;
+    uint32_t item_chunks, groups, bulk_chunks, tail_chunks;
+    uint32_t rb_shift;      // log2(row_block) when it is a power of two, else 32
     // LDS layout of the scene-staging kernels (byte offsets / 16-byte padded sizes)
     uint32_t lds_nodes, lds_refs, lds_spheres, lds_quads, lds_stack;
     uint32_t bytes_nodes, bytes_refs, bytes_spheres, bytes_quads;
@@ -968,7 +967,11 @@ __device__ __forceinline__ void leaf_step(const SceneView& S, Stack<SE>& st, con
 }
 
 __device__ __forceinline__ uint32_t owned_row(const Work& w, uint32_t k) {
-    uint32_t blk = k / w.row_block, in = k % w.row_block;
+    if (w.rb_shift < 32) {  // power-of-two row blocks: no division
+        const uint32_t blk = k >> w.rb_shift, in = k & ((1u << w.rb_shift) - 1);
+        return ((blk * w.tile_count + w.tile_index) << w.rb_shift) | in;
+    }
+    const uint32_t blk = k / w.row_block, in = k % w.row_block;
     return (blk * w.tile_count + w.tile_index) * w.row_block + in;
 }
 
@@ -1113,11 +1116,11 @@ __device__ __forceinline__ void stage_lds(unsigned char* dst, const void* src, u
     for (uint32_t i = threadIdx.x; i < bytes / 16; i += kBlock) d[i] = s[i];
 }
 
-// The render kernel. Block -> (8x8 pixel tile, a range of sample chunks): a pool of 64 x (its
-// chunks) (chunk, pixel) units that the lanes of the block's waves draw from as they finish
-// them, so the waves of a block finish together (the block's LDS and wave slots are released
-// only when all of them are done). The blocks dispatched last own fewer chunks
-// (Work::tail_pool_chunks), so the kernel drains quickly.
+// The render kernel: a persistent grid (as many blocks as are resident) whose waves take work
+// items from a queue in HBM, one atomic per item: item = (8x8 pixel tile, sample chunk), 64
+// (chunk, pixel) units, in tile-major order. A wave's lanes draw units as they finish one,
+// crossing from one item into the next without waiting, so a lane idles only once the queue is
+// dry, and the grid drains within about one unit.
 // Persistent per-lane state machine (WALK -> LEAF -> ... -> DONE -> shade -> WALK) in traversal
 // rounds: every walking lane walks the DFS to its next entered leaf (or the end of its
 // traversal), then the lanes holding a leaf test it together. Lanes whose ray is finished park
@@ -1186,30 +1189,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LSCENE ?
     }
     // The camera constants are read from an LDS copy in start_path / shade: held in SGPRs for
     // the whole kernel they would spill (into VGPR lanes, reloaded with v_readlane per use).
-    // block-uniform (SGPRs): the tile coordinates stay live for the whole kernel
-    const uint64_t block = blockIdx.x;
-    uint32_t tile, chunk0, nch;
-    if (block < W.bulk_blocks) {
-        tile = static_cast<uint32_t>(block / W.groups);
-        chunk0 = static_cast<uint32_t>(block % W.groups) * W.pool_chunks;
-        nch = W.pool_chunks;
-    } else {
-        const uint64_t b2 = block - W.bulk_blocks;
-        tile = static_cast<uint32_t>(b2 / W.tail_groups);
-        chunk0 = W.bulk_chunks + static_cast<uint32_t>(b2 % W.tail_groups) * W.tail_pool_chunks;
-        nch = W.tail_pool_chunks;
-    }
-    if (W.tile_order == 1) tile = W.tiles - 1 - tile;
-    else if (W.tile_order == 2) tile = static_cast<uint32_t>((static_cast<uint64_t>(tile) * W.tile_stride) % W.tiles);
-    const uint32_t tx = tile % W.tiles_x, ty = tile / W.tiles_x;
-    // LDS: the pool counter, then the image rows of the tile's 8 owned rows (owned_row divides)
-    uint32_t* const pool_next = reinterpret_cast<uint32_t*>(smem + W.lds_pool);
-    uint32_t* const tile_rows = pool_next + 4;
-    if (threadIdx.x == 0) {
-        *reinterpret_cast<CamView*>(smem + W.lds_cam) = C;
-        *pool_next = 0;
-    }
-    if (threadIdx.x < 8) tile_rows[threadIdx.x] = owned_row(W, ty * 8 + threadIdx.x);
+    if (threadIdx.x == 0) *reinterpret_cast<CamView*>(smem + W.lds_cam) = C;
     __syncthreads();
     const CamView& CL = *reinterpret_cast<const CamView*>(smem + W.lds_cam);
     const float tmin32 = W.tmin32;  // a kernel argument (SGPR): no conversion in the walk loop
@@ -1228,14 +1208,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LSCENE ?
         st.stride = kBlock;
     }
     st.base[-static_cast<ptrdiff_t>(st.stride)] = static_cast<SE>(W.sentinel);
-    // The block's pool of work units: unit u = (chunk chunk0 + u / 64, pixel u % 64 of the
-    // tile), in that order. Lanes that finish a unit take the next ones (one LDS atomic per wave
-    // and draw, then in lane order), so no lane idles until the pool is dry; a unit's sum goes to
-    // partial[chunk][pixel] whichever lane traced it, so frames do not depend on the schedule.
-    const uint32_t pool = 64 * nch;
-    // the lane's unit and sample; its chunk, tile pixel and row are recomputed where needed
-    // (kept live across the phases they would spill)
-    uint32_t u = 0, s = 0;
+    // The wave's current item (wave-uniform) and how many of its 64 units are drawn; lanes take
+    // the next units in lane order. A unit's sum goes to partial[chunk][pixel] whichever lane
+    // traced it, so frames do not depend on the schedule.
+    uint32_t item = 0, item_pos = 0, item_units = 0;
+    uint32_t item_txy = 0, item_chunk = 0;
+    // the lane's unit: tile (tx | ty << 16), chunk << 6 | tile pixel; and its current sample
+    uint32_t u_txy = 0, u_cp = 0, s = 0;
     double acc[3] = {0, 0, 0};
     Path P;
     Trav R;
@@ -1244,42 +1223,65 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LSCENE ?
     uint32_t cw = 0, cl = 0, cs = 0;  // wall_clock64 ticks (100 MHz), differences mod 2^32
     unsigned long long t_first_idle = 0;
     while (true) {
-        // lanes without a unit draw from the pool until each holds a unit with samples to trace
-        // or the pool is dry. A unit off the image or past spp has no pixel sum; one with
-        // max_depth == 0 sums RGB::zero() (camera.h:211-213) and is written at once.
+        // lanes without a unit draw until each holds a unit with samples to trace or the queue
+        // is dry. A unit off the image has no pixel sum; one with max_depth == 0 sums
+        // RGB::zero() (camera.h:211-213) and is written at once.
         while (true) {
             const uint64_t m = __ballot(need);
             if (m == 0) break;
-            const uint32_t leader = static_cast<uint32_t>(__ffsll(static_cast<long long>(m)) - 1);
-            uint32_t base = 0;
-            if (lane == leader) base = atomicAdd(pool_next, static_cast<uint32_t>(__popcll(m)));
-            base = __builtin_amdgcn_readlane(base, leader);
-            if (need) {
-                u = base + __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32),
-                                                     __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0u));
-                if (u >= pool) {
-                    need = false;
-                } else {
-                    const uint32_t chunk = chunk0 + (u >> 6);
-                    const uint32_t col = tx * 8 + (u & 7), k = ty * 8 + ((u >> 3) & 7);
-                    if (chunk < W.chunks && col < C.w && k < W.owned_rows) {
-                        s = chunk * W.chunk_len;
-                        if (C.max_depth > 0) {
-                            need = false;
-                            start = true;
-                        } else if (!COUNT) {
-                            double* dst = partial + (static_cast<size_t>(chunk) * W.owned_rows * C.w +
-                                                     static_cast<size_t>(k) * C.w + col) * 3;
-                            dst[0] = 0;
-                            dst[1] = 0;
-                            dst[2] = 0;
-                        }
+            if (item_pos >= item_units) {  // the item is used up: the next one from the queue
+                const uint32_t leader = static_cast<uint32_t>(__ffsll(static_cast<long long>(m)) - 1);
+                uint32_t v = 0;
+                if (lane == leader) v = atomicAdd(W.queue, 1u);
+                item = __builtin_amdgcn_readlane(v, leader);
+                item_pos = 0;
+                if (item < W.n_items) {
+                    uint32_t tile;
+                    if (item < W.bulk_items) {
+                        tile = item / W.groups;
+                        item_chunk = (item - tile * W.groups) * W.item_chunks;
+                        item_units = 64 * W.item_chunks;
+                    } else {
+                        const uint32_t j = item - W.bulk_items;
+                        tile = j / W.tail_chunks;
+                        item_chunk = W.bulk_chunks + (j - tile * W.tail_chunks);
+                        item_units = 64;
+                    }
+                    item_txy = (tile % W.tiles_x) | ((tile / W.tiles_x) << 16);
+                }
+            }
+            if (item >= W.n_items) {  // the queue is dry
+                need = false;
+                break;
+            }
+            const uint32_t take = min(static_cast<uint32_t>(__popcll(m)), item_units - item_pos);
+            const uint32_t r = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32),
+                                                         __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0u));
+            if (need && r < take) {
+                const uint32_t uu = item_pos + r, pix = uu & 63, chunk = item_chunk + (uu >> 6);
+                u_txy = item_txy;
+                u_cp = (chunk << 6) | pix;
+                const uint32_t col = (item_txy & 0xffffu) * 8 + (pix & 7), k = (item_txy >> 16) * 8 + (pix >> 3);
+                if (chunk < W.chunks && col < C.w && k < W.owned_rows) {
+                    s = chunk * W.chunk_len;
+                    if (C.max_depth > 0) {
+                        need = false;
+                        start = true;
+                    } else if (!COUNT) {
+                        double* dst = partial + (static_cast<size_t>(chunk) * W.owned_rows * C.w +
+                                                 static_cast<size_t>(k) * C.w + col) * 3;
+                        dst[0] = 0;
+                        dst[1] = 0;
+                        dst[2] = 0;
                     }
                 }
             }
+            item_pos += take;
         }
         if (start) {
-            const uint32_t col = tx * 8 + (u & 7), row = tile_rows[(u >> 3) & 7];
+            const uint32_t pix = u_cp & 63;
+            const uint32_t col = (u_txy & 0xffffu) * 8 + (pix & 7);
+            const uint32_t row = owned_row(W, (u_txy >> 16) * 8 + (pix >> 3));
             start_path(CL, row, col, sample_seed(C.base_seed, row * C.w + col, s), P);
         }
         // one traversal set-up for new samples and scattered rays alike (the wave runs it once);
@@ -1322,12 +1324,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LSCENE ?
             if (!ended) {
                 cont = true;  // the scattered ray: traversal set-up with the new samples' (above)
             } else {
-                const uint32_t chunk = chunk0 + (u >> 6);
+                const uint32_t chunk = u_cp >> 6;
                 if (++s < min(C.spp, (chunk + 1) * W.chunk_len)) {
                     start = true;  // the unit's next sample (started after the draw, with the drawers)
                 } else {  // the unit is done: its sum (samples in order) to partial[chunk][pixel]
                     if (!COUNT) {
-                        const uint32_t col = tx * 8 + (u & 7), k = ty * 8 + ((u >> 3) & 7);
+                        const uint32_t pix = u_cp & 63;
+                        const uint32_t col = (u_txy & 0xffffu) * 8 + (pix & 7), k = (u_txy >> 16) * 8 + (pix >> 3);
                         double* dst = partial + (static_cast<size_t>(chunk) * W.owned_rows * C.w +
                                                  static_cast<size_t>(k) * C.w + col) * 3;
                         dst[0] = acc[0];
@@ -1662,58 +1665,54 @@ static int launch_render(const crt_scene* s, int device, const crt_camera* cam, 
     const DeviceCopy& c = s->dev[device];
     dev::Work W = w0;
     W.lds_cam = static_cast<uint32_t>(align16(lds));  // the camera copy after the rest
-    W.lds_pool = static_cast<uint32_t>(W.lds_cam + align16(sizeof(dev::CamView)));
-    lds = W.lds_pool + 48;  // pool counter (16 B) + the tile's 8 image rows
+    lds = W.lds_cam + align16(sizeof(dev::CamView));
     const uint64_t pixels = static_cast<uint64_t>(W.owned_rows) * cam->image_w;
     // Sample chunks: a function of spp ONLY, so every pixel's sum is grouped identically whatever
-    // the tiling / number of GPUs / block pools / lane schedule (bit-identical frames for 1..N
-    // devices): 8 samples, or spp / 192 above 1536 spp. A block owns a pool of chunks of one 8x8
-    // tile (64 units per chunk, drawn by the lanes of its 4 waves as they finish one). On a whole
-    // frame, per tile one bulk block takes 8/9 of the chunks (56 of 63 at BASELINE spp), and one
-    // tail block the rest; all tail blocks are dispatched after all bulk blocks, so the kernel
-    // ends on short blocks. Measured on config 2 (Msamples/s, bulk/tail chunks): 56/7 4470, 48/15 4430,
-    // 63/0 4273, 24+24/15 4335, 12x5/3 4087; waves with private 3-chunk pools 4108.
-    // CRT_POOL_CHUNKS, CRT_TAIL_CHUNKS and CRT_TAIL_POOL_CHUNKS (environment) override the split;
-    // frames do not change.
+    // the tiling / number of GPUs / lane schedule (bit-identical frames for 1..N devices): 8
+    // samples, or spp / 192 above 1536 spp. The persistent grid's waves take (tile, chunk) items
+    // from a queue in tile-major order (render_kernel).
     const uint32_t spp = cam->samples_per_pixel;
 #ifndef CRT_CHUNK_MIN
 #define CRT_CHUNK_MIN 8
 #endif
-    auto knob = [](const char* name, uint32_t dflt) {
-        const char* e = std::getenv(name);
-        return e ? static_cast<uint32_t>(std::max(0, std::min(4096, std::atoi(e)))) : dflt;
-    };
     W.chunk_len = std::max<uint32_t>(CRT_CHUNK_MIN, (spp + 191) / 192);
     W.chunks = (spp + W.chunk_len - 1) / W.chunk_len;
-    // Default split: bpt bulk blocks per tile, bpt = 1 when the tiles fill CRT_BLOCK_ROUNDS (4)
-    // rounds of resident blocks, else as many as needed for that (a GPU's share of a multi-GPU
-    // frame). With 1 or 2 bulk blocks they take 8/9 of the chunks and one tail block the rest
-    // (config 2: 56+7 chunks on one GPU, 28+28+7 at 4 GPUs); with more, the blocks are already
-    // short and split the chunks evenly (at 8 GPUs 21+21+21; 18+18+18+9 was slower).
-    // Four rounds at 5 blocks/CU (the LDS-scene kernels) are ~5000 blocks, as five were at 4.
-    // tools/tile_timing.py, per-rank ms at N = 1/2/4/8: 91.9/49.5/27.1/16.0.
+    W.rb_shift = 32;
+    for (uint32_t sh = 0; sh < 31; ++sh)
+        if ((1u << sh) == W.row_block) W.rb_shift = sh;
+    // the grid: every resident block (more would only wait), fewer when the items are fewer
     int cus = 0, per_cu = 0;
     HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
     HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(
         &per_cu, reinterpret_cast<const void*>(dev::render_kernel<SE, GSTACK, LSCENE, false>), dev::kBlock, lds));
-    const uint64_t target = static_cast<uint64_t>(knob("CRT_BLOCK_ROUNDS", 4)) * std::max(1, cus) * std::max(1, per_cu);
-    const uint32_t bpt = static_cast<uint32_t>(std::min<uint64_t>(W.chunks, (target + W.tiles - 1) / std::max<uint32_t>(1, W.tiles)));
-    const uint32_t nb = std::max<uint32_t>(1, bpt);
-    const uint32_t pool_dflt = nb <= 2 ? std::max<uint32_t>(1, (W.chunks - W.chunks / 9) / nb) : (W.chunks + nb - 1) / nb;
-    const uint32_t tail_dflt = nb <= 2 ? W.chunks - nb * pool_dflt : 0;
-    const uint32_t tail = std::min(W.chunks, knob("CRT_TAIL_CHUNKS", tail_dflt));
-    W.pool_chunks = std::max<uint32_t>(1, knob("CRT_POOL_CHUNKS", pool_dflt));
-    W.groups = (W.chunks - tail) / W.pool_chunks;
-    W.bulk_chunks = W.groups * W.pool_chunks;
-    // the tail: every chunk the bulk blocks leave, in one block per tile by default
-    W.tail_pool_chunks = std::max<uint32_t>(1, knob("CRT_TAIL_POOL_CHUNKS", W.chunks - W.bulk_chunks));
-    W.tail_groups = (W.chunks - W.bulk_chunks + W.tail_pool_chunks - 1) / W.tail_pool_chunks;
-    W.bulk_blocks = static_cast<uint64_t>(W.tiles) * W.groups;
-    W.tile_order = knob("CRT_TILE_ORDER", 0);
-    W.tile_stride = 7919;  // prime: tile * stride mod tiles is a permutation unless 7919 | tiles
-    if (W.tile_order == 2 && W.tiles % W.tile_stride == 0) W.tile_order = 0;
-    const uint64_t blocks = W.bulk_blocks + static_cast<uint64_t>(W.tiles) * W.tail_groups;
-    if (blocks > 0x7fffffffull) return fail(CRT_E_INVALID, "frame too large for one launch");
+    constexpr uint32_t kWavesPerBlock = dev::kBlock / 64;
+    uint64_t blocks = std::max<uint64_t>(1, std::min<uint64_t>(static_cast<uint64_t>(std::max(1, cus)) * std::max(1, per_cu),
+                                                               (static_cast<uint64_t>(W.tiles) * W.chunks + kWavesPerBlock - 1) / kWavesPerBlock));
+    if (const char* e = std::getenv("CRT_GRID_BLOCKS"))  // schedule tests: a smaller grid, same frame
+        blocks = std::max<uint64_t>(1, std::min<uint64_t>(blocks, static_cast<uint64_t>(std::max(1, std::atoi(e)))));
+    // Items: bulk items of K chunks for the first 8/9 of each tile's chunks, then the rest in
+    // one-chunk items at the end of the queue (CRT_TAIL_CHUNKS), so the grid drains on small
+    // items; a wave's lanes cross from item to item without waiting either way. K keeps an item
+    // small against a wave's share of the frame (a tile costs up to ~10x another): a 26th of
+    // the units per lane, at most 7 (config 2: 7 on one GPU, 3/1/1 for a rank's share at 2/4/8
+    // GPUs; no tail items with K = 1). Measured on config 2, one GPU (Msamples/s): K = 1 5127,
+    // 7 5273, 14 4828, 28 4025; a rank's share at 4 / 8 GPUs took 24.8 / 14.1 ms with K = 1,
+    // 26.1 / 19.4 with K = 2 / 7 (CRT_ITEM_CHUNKS, CRT_TAIL_CHUNKS override).
+    auto knob = [](const char* name, uint32_t dflt) {
+        const char* e = std::getenv(name);
+        return e ? static_cast<uint32_t>(std::max(0, std::min(4096, std::atoi(e)))) : dflt;
+    };
+    const uint64_t per_lane = static_cast<uint64_t>(W.tiles) * W.chunks / (blocks * kWavesPerBlock);
+    W.item_chunks = std::max<uint32_t>(1, knob("CRT_ITEM_CHUNKS", static_cast<uint32_t>(std::min<uint64_t>(7, std::max<uint64_t>(1, per_lane / 26)))));
+    const uint32_t tail_want = std::min(W.chunks, knob("CRT_TAIL_CHUNKS", W.item_chunks > 1 ? W.chunks / 9 : 0));
+    W.groups = (W.chunks - tail_want) / W.item_chunks;
+    W.bulk_chunks = W.groups * W.item_chunks;
+    W.tail_chunks = W.chunks - W.bulk_chunks;
+    const uint64_t bulk_items = static_cast<uint64_t>(W.tiles) * W.groups;
+    const uint64_t items = bulk_items + static_cast<uint64_t>(W.tiles) * W.tail_chunks;
+    if (items >= 0xffffffffull) return fail(CRT_E_INVALID, "frame too large for one launch");
+    W.n_items = static_cast<uint32_t>(items);
+    W.bulk_items = static_cast<uint32_t>(bulk_items);
     const size_t plane = static_cast<size_t>(pixels) * 3;  // partials indexed by owned pixel
 
     double* partial = nullptr;
@@ -1730,6 +1729,10 @@ static int launch_render(const crt_scene* s, int device, const crt_camera* cam, 
         HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&ctr), sizeof(dev::Counters), stream));
         HIP_TRY(hipMemsetAsync(ctr, 0, sizeof(dev::Counters), stream));
     }
+    uint32_t* queue = nullptr;
+    HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&queue), 256, stream));
+    HIP_TRY(hipMemsetAsync(queue, 0, sizeof(uint32_t), stream));
+    W.queue = queue;
     dev::SceneView S = view_of(c);
     dev::CamView C = cam_view(cam);
     hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -1753,6 +1756,7 @@ static int launch_render(const crt_scene* s, int device, const crt_camera* cam, 
         }
     }
     if (partial) HIP_TRY(hipFreeAsync(partial, stream));
+    HIP_TRY(hipFreeAsync(queue, stream));
     if (gstack) HIP_TRY(hipFreeAsync(gstack, stream));
     if (count) {
         dev::Counters h{};

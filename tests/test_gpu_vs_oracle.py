@@ -141,18 +141,16 @@ def test_f32_decisions_equal_f64(crt, monkeypatch, name, seed, kw):
 
 
 @pytest.mark.parametrize("spp", [40, 2000])
-def test_block_pools_do_not_change_frames(crt, monkeypatch, spp):
-    """Which block traces which (chunk, pixel) unit, and when, does not enter the result: the
+def test_work_queue_schedule_does_not_change_frames(crt, monkeypatch, spp):
+    """Which wave traces which (chunk, pixel) unit, and when, does not enter the result: the
     chunk length depends on spp only and each unit's sum lands in its own partial slot. Frames
-    under different bulk / tail pool splits (CRT_POOL_CHUNKS, CRT_TAIL_CHUNKS,
-    CRT_TAIL_POOL_CHUNKS) are bit-identical, including a half-empty last tile row."""
+    from persistent grids of 1, 3 and 37 blocks (CRT_GRID_BLOCKS) and the full grid are
+    bit-identical, including a half-empty last tile row."""
     d = scene(crt, "rtow_final", 42, image_w=120, image_h=84, samples_per_pixel=spp, max_depth=20)
     base = gpu(crt, d, 43)
-    for pool, tail, tpool in [(1, 2, 2), (3, 0, 1), (1000, 0, 1), (2, 5, 3)]:
-        monkeypatch.setenv("CRT_POOL_CHUNKS", str(pool))
-        monkeypatch.setenv("CRT_TAIL_CHUNKS", str(tail))
-        monkeypatch.setenv("CRT_TAIL_POOL_CHUNKS", str(tpool))
-        assert np.array_equal(base, gpu(crt, d, 43)), (pool, tail, tpool)
+    for blocks in (1, 3, 37):
+        monkeypatch.setenv("CRT_GRID_BLOCKS", str(blocks))
+        assert np.array_equal(base, gpu(crt, d, 43)), blocks
 
 
 @pytest.mark.parametrize("name,seed", [("rtow_final", 42), ("cornell", None), ("christmas_tree", None),
