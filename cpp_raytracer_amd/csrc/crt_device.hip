@@ -1134,10 +1134,11 @@ __device__ __forceinline__ void stage_lds(unsigned char* dst, const void* src, u
 #ifndef CRT_WAVES_PER_EU
 #define CRT_WAVES_PER_EU 4
 #endif
-// LDS-scene kernels: 5 waves per SIMD (96 VGPRs, ~55 spilled) measured +0.7% on config 2 and
-// +1.2% on config 3; the HBM-scene kernels lose 14% with it (config 4) and keep 4
+// LDS-scene kernels: 5 waves per SIMD (96 VGPRs) spill 65 VGPRs with the work-queue state and
+// wrote 94 GB of scratch per config-2 frame: 5262 vs 5499 Msamples/s at 4 (config 3: 1958 vs
+// 1939); with v10's block pools 5 had measured +0.7%. The HBM-scene kernels lose 14% at 5.
 #ifndef CRT_WAVES_PER_EU_LDS
-#define CRT_WAVES_PER_EU_LDS 5
+#define CRT_WAVES_PER_EU_LDS 4
 #endif
 #ifndef CRT_SHADE_BATCH
 #define CRT_SHADE_BATCH 48
@@ -1693,7 +1694,7 @@ static int launch_render(const crt_scene* s, int device, const crt_camera* cam, 
     // Items: bulk items of K chunks for the first 8/9 of each tile's chunks, then the rest in
     // one-chunk items at the end of the queue (CRT_TAIL_CHUNKS), so the grid drains on small
     // items; a wave's lanes cross from item to item without waiting either way. K keeps an item
-    // small against a wave's share of the frame (a tile costs up to ~10x another): a 26th of
+    // small against a wave's share of the frame (a tile costs up to ~10x another): a 30th of
     // the units per lane, at most 7 (config 2: 7 on one GPU, 3/1/1 for a rank's share at 2/4/8
     // GPUs; no tail items with K = 1). Measured on config 2, one GPU (Msamples/s): K = 1 5127,
     // 7 5273, 14 4828, 28 4025; a rank's share at 4 / 8 GPUs took 24.8 / 14.1 ms with K = 1,
@@ -1703,7 +1704,7 @@ static int launch_render(const crt_scene* s, int device, const crt_camera* cam, 
         return e ? static_cast<uint32_t>(std::max(0, std::min(4096, std::atoi(e)))) : dflt;
     };
     const uint64_t per_lane = static_cast<uint64_t>(W.tiles) * W.chunks / (blocks * kWavesPerBlock);
-    W.item_chunks = std::max<uint32_t>(1, knob("CRT_ITEM_CHUNKS", static_cast<uint32_t>(std::min<uint64_t>(7, std::max<uint64_t>(1, per_lane / 26)))));
+    W.item_chunks = std::max<uint32_t>(1, knob("CRT_ITEM_CHUNKS", static_cast<uint32_t>(std::min<uint64_t>(7, std::max<uint64_t>(1, per_lane / 30)))));
     const uint32_t tail_want = std::min(W.chunks, knob("CRT_TAIL_CHUNKS", W.item_chunks > 1 ? W.chunks / 9 : 0));
     W.groups = (W.chunks - tail_want) / W.item_chunks;
     W.bulk_chunks = W.groups * W.item_chunks;
