@@ -36,6 +36,13 @@ namespace dev {
 #define CRT_BLOCK 256
 #endif
 constexpr int kBlock = CRT_BLOCK;
+// pixel tile of one work item's 64 units (kTileW x kTileH owned rows): 16 x 4 matches the
+// multi-GPU bench's 4-row blocks, so a tile is contiguous on the image at any GPU count
+// (per-rank share at 8 GPUs 13.0 vs 13.2 ms for 8 x 8; one GPU 87.5 vs 87.0)
+#ifndef CRT_TILE_W
+#define CRT_TILE_W 16
+#endif
+constexpr uint32_t kTileW = CRT_TILE_W, kTileH = 64 / CRT_TILE_W;
 constexpr double kScale = 1 / static_cast<double>(4294967295u - 1);  // rand_util.h:110-112
 
 typedef double Dvec2 __attribute__((ext_vector_type(2)));
@@ -1262,7 +1269,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LSCENE ?
                 const uint32_t uu = item_pos + r, pix = uu & 63, chunk = item_chunk + (uu >> 6);
                 u_txy = item_txy;
                 u_cp = (chunk << 6) | pix;
-                const uint32_t col = (item_txy & 0xffffu) * 8 + (pix & 7), k = (item_txy >> 16) * 8 + (pix >> 3);
+                const uint32_t col = (item_txy & 0xffffu) * kTileW + pix % kTileW, k = (item_txy >> 16) * kTileH + pix / kTileW;
                 if (chunk < W.chunks && col < C.w && k < W.owned_rows) {
                     s = chunk * W.chunk_len;
                     if (C.max_depth > 0) {
@@ -1281,8 +1288,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LSCENE ?
         }
         if (start) {
             const uint32_t pix = u_cp & 63;
-            const uint32_t col = (u_txy & 0xffffu) * 8 + (pix & 7);
-            const uint32_t row = owned_row(W, (u_txy >> 16) * 8 + (pix >> 3));
+            const uint32_t col = (u_txy & 0xffffu) * kTileW + pix % kTileW;
+            const uint32_t row = owned_row(W, (u_txy >> 16) * kTileH + pix / kTileW);
             start_path(CL, row, col, sample_seed(C.base_seed, row * C.w + col, s), P);
         }
         // one traversal set-up for new samples and scattered rays alike (the wave runs it once);
@@ -1315,7 +1322,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LSCENE ?
         }
         const uint64_t m_done = __ballot(R.state == kDone);
         if (COUNT && t_first_idle == 0 && __ballot(R.state == kIdle) != 0) t_first_idle = wall_clock64();
-        if (m_done == 0) break;  // every lane idle: the pool is dry
+        if (m_done == 0) break;  // every lane idle: the queue is dry
         if (COUNT) cs -= static_cast<uint32_t>(wall_clock64());
         if (R.state == kDone) {
             if (COUNT && wave_leader()) ctr.it_shade++;
@@ -1331,7 +1338,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LSCENE ?
                 } else {  // the unit is done: its sum (samples in order) to partial[chunk][pixel]
                     if (!COUNT) {
                         const uint32_t pix = u_cp & 63;
-                        const uint32_t col = (u_txy & 0xffffu) * 8 + (pix & 7), k = (u_txy >> 16) * 8 + (pix >> 3);
+                        const uint32_t col = (u_txy & 0xffffu) * kTileW + pix % kTileW, k = (u_txy >> 16) * kTileH + pix / kTileW;
                         double* dst = partial + (static_cast<size_t>(chunk) * W.owned_rows * C.w +
                                                  static_cast<size_t>(k) * C.w + col) * 3;
                         dst[0] = acc[0];
@@ -1669,12 +1676,14 @@ static int launch_render(const crt_scene* s, int device, const crt_camera* cam, 
     lds = W.lds_cam + align16(sizeof(dev::CamView));
     const uint64_t pixels = static_cast<uint64_t>(W.owned_rows) * cam->image_w;
     // Sample chunks: a function of spp ONLY, so every pixel's sum is grouped identically whatever
-    // the tiling / number of GPUs / lane schedule (bit-identical frames for 1..N devices): 8
-    // samples, or spp / 192 above 1536 spp. The persistent grid's waves take (tile, chunk) items
+    // the tiling / number of GPUs / lane schedule (bit-identical frames for 1..N devices): 4
+    // samples, or spp / 192 above 768 spp. A unit is the grain the grid drains on: per-rank share
+    // at 8 GPUs 12.2 ms with 4-sample chunks vs 13.0 with 8 (one GPU 87.4 vs 87.5; the partial
+    // sums double to 2.9 GB per config-2 frame). The persistent grid's waves take (tile, chunk) items
     // from a queue in tile-major order (render_kernel).
     const uint32_t spp = cam->samples_per_pixel;
 #ifndef CRT_CHUNK_MIN
-#define CRT_CHUNK_MIN 8
+#define CRT_CHUNK_MIN 4
 #endif
     W.chunk_len = std::max<uint32_t>(CRT_CHUNK_MIN, (spp + 191) / 192);
     W.chunks = (spp + W.chunk_len - 1) / W.chunk_len;
@@ -1883,8 +1892,8 @@ int device_render(const crt_scene* s, int device, const crt_camera* cam, const c
         }
         return CRT_OK;
     }
-    W.tiles_x = (cam->image_w + 7) / 8;
-    W.tiles_y = (W.owned_rows + 7) / 8;
+    W.tiles_x = (cam->image_w + dev::kTileW - 1) / dev::kTileW;
+    W.tiles_y = (W.owned_rows + dev::kTileH - 1) / dev::kTileH;
     W.tiles = W.tiles_x * W.tiles_y;
     W.sphere_only = (s->quads.empty() && !s->spheres.empty()) ? 1u : 0u;
     W.spheres_f32 = (W.sphere_only && s->dev[device].spheres_f32_ok) ? 1u : 0u;
