@@ -60,6 +60,9 @@ struct SceneView {
     const DevQuad* quads;
     const uint32_t* quad_mat;
     const DevMaterial* mats;
+    // LSCENE kernels: LDS byte offsets of the staged refs / f64 spheres / parallelograms, read
+    // through typed LDS pointers (ds_read, not flat); spheres_lds = ~0u when the spheres stay in HBM
+    uint32_t refs_lds, spheres_lds, quads_lds;
 };
 
 struct CamView {
@@ -438,6 +441,21 @@ __device__ __forceinline__ DevSphere sphere_global(const DevSphere* p) {
     r.c[0] = a.x; r.c[1] = a.y; r.c[2] = b.x; r.r = b.y;
     return r;
 }
+// a 16-byte aligned record (DevSphere, DevQuad, u32) at an LDS byte offset, read as ds_read
+typedef __attribute__((address_space(3))) const Dvec2 LdsDvec2;
+template <typename T>
+__device__ __forceinline__ T lds_rec(uint32_t off) {
+    static_assert(sizeof(T) % 16 == 0, "16-byte lines");
+    T r;
+    Dvec2* dst = reinterpret_cast<Dvec2*>(&r);
+    const LdsDvec2* src = (LdsDvec2*)static_cast<uintptr_t>(off);
+#pragma unroll
+    for (uint32_t k = 0; k < sizeof(T) / 16; ++k) dst[k] = src[k];
+    return r;
+}
+__device__ __forceinline__ uint32_t lds_u32(uint32_t off) {
+    return *(__attribute__((address_space(3))) const uint32_t*)static_cast<uintptr_t>(off);
+}
 // the verdicts of the record's two spheres: bit 1 = first, bit 0 = second (1 = candidate)
 __device__ __forceinline__ uint32_t sphere_pair_candidates(const DevSpherePair& sp, const LeafRay32& L) {
     const F2 cx = {sp.cx[0], sp.cx[1]}, cy = {sp.cy[0], sp.cy[1]}, cz = {sp.cz[0], sp.cz[1]};
@@ -479,7 +497,15 @@ __device__ __forceinline__ bool hit_quad(const DevQuad& q, const double o[3], co
     return false;
 }
 
+// sphere i: LS kernels read the LDS copy or, in the f32-filter mode, HBM through a typed pointer
+template <bool LS>
+__device__ __forceinline__ DevSphere sphere_at(const SceneView& S, uint32_t i) {
+    if (!LS) return S.spheres[i];
+    return S.spheres_lds != ~0u ? lds_rec<DevSphere>(S.spheres_lds + (i << 5)) : sphere_global(S.spheres + i);
+}
+
 // Resolve the hit record (hittable.h:46-71): hit point ray(t), outward normal, front face.
+template <bool LS>
 __device__ __forceinline__ uint32_t hit_record(const SceneView& S, uint32_t ref, const double o[3],
                                                const double d[3], double t, double p[3],
                                                double nrm[3], bool& front) {
@@ -489,15 +515,23 @@ __device__ __forceinline__ uint32_t hit_record(const SceneView& S, uint32_t ref,
     double nx, ny, nz;
     uint32_t m;
     if (ref & kRefQuad) {
-        const DevQuad& q = S.quads[ref & ~kRefQuad];
-        nx = q.n[0]; ny = q.n[1]; nz = q.n[2];
+        if constexpr (LS) {
+            const DevQuad q = lds_rec<DevQuad>(S.quads_lds + ((ref & ~kRefQuad) << 7));
+            nx = q.n[0]; ny = q.n[1]; nz = q.n[2];
+        } else {
+            const DevQuad& q = S.quads[ref & ~kRefQuad];
+            nx = q.n[0]; ny = q.n[1]; nz = q.n[2];
+        }
         m = S.quad_mat[ref & ~kRefQuad];
     } else {
-        const DevSphere& sp = S.spheres[ref];
-        const double ir = 1 / sp.r;  // (hit_point - center) / radius
-        nx = (p[0] - sp.c[0]) * ir;
-        ny = (p[1] - sp.c[1]) * ir;
-        nz = (p[2] - sp.c[2]) * ir;
+        const auto normal = [&](const DevSphere& sp) {
+            const double ir = 1 / sp.r;  // (hit_point - center) / radius
+            nx = (p[0] - sp.c[0]) * ir;
+            ny = (p[1] - sp.c[1]) * ir;
+            nz = (p[2] - sp.c[2]) * ir;
+        };
+        if constexpr (LS) normal(sphere_at<LS>(S, ref));
+        else normal(S.spheres[ref]);
         m = S.sphere_mat[ref];
     }
     if (d[0] * nx + d[1] * ny + d[2] * nz > 0) {
@@ -928,11 +962,11 @@ __device__ __forceinline__ void leaf_step(const SceneView& S, Stack<SE>& st, con
             }
         }
     } else if (sphere_only) {
-        DevSphere cur = S.spheres[range.x];
+        DevSphere cur = sphere_at<LS>(S, range.x);
         for (uint32_t i = range.x; i < end; ++i) {
             // one past the leaf's last sphere is still inside the scene copy (sphere_mat follows
             // the spheres in HBM, the parallelogram / stack regions in LDS); it is never tested
-            const DevSphere nxt = S.spheres[i + 1];
+            const DevSphere nxt = sphere_at<LS>(S, i + 1);
             if (COUNT) {
                 ctr.sphere_tests++;
                 if (wave_leader()) ctr.it_leaf++;
@@ -949,16 +983,19 @@ __device__ __forceinline__ void leaf_step(const SceneView& S, Stack<SE>& st, con
         }
     } else {
         for (uint32_t i = range.x; i < end; ++i) {
-            const uint32_t ref = S.refs[i];
+            // LS: refs, spheres and parallelograms are all staged (spheres_f32 is off here)
+            const uint32_t ref = LS ? lds_u32(S.refs_lds + (i << 2)) : S.refs[i];
             double t;
             bool h;
             if (COUNT && wave_leader()) ctr.it_leaf++;
             if (ref & kRefQuad) {
                 if (COUNT) ctr.quad_tests++;
-                h = hit_quad(S.quads[ref & ~kRefQuad], o, d, tmin, R.tmax, t);
+                if constexpr (LS) h = hit_quad(lds_rec<DevQuad>(S.quads_lds + ((ref & ~kRefQuad) << 7)), o, d, tmin, R.tmax, t);
+                else h = hit_quad(S.quads[ref & ~kRefQuad], o, d, tmin, R.tmax, t);
             } else {
                 if (COUNT) ctr.sphere_tests++;
-                h = hit_sphere(S.spheres[ref], o, d, R.a, ia, tmin, R.tmax, lo, hi, t);
+                if constexpr (LS) h = hit_sphere(lds_rec<DevSphere>(S.spheres_lds + (ref << 5)), o, d, R.a, ia, tmin, R.tmax, lo, hi, t);
+                else h = hit_sphere(S.spheres[ref], o, d, R.a, ia, tmin, R.tmax, lo, hi, t);
             }
             if (h) {
                 R.tmax = t;
@@ -1029,6 +1066,7 @@ __device__ __forceinline__ void start_path(const CamView& C, uint32_t row, uint3
 // One level of ray_color (camera.h:205-258) after the closest-hit query: scatters
 // (material.h:64-263) into the next ray, or ends the path adding T * (background | emission) to
 // acc. Returns true when the path has ended (miss, light, absorption).
+template <bool LS>
 __device__ __forceinline__ bool shade(const SceneView& S, const CamView& C, Path& P, bool hit,
                                       uint32_t ref, double t, double acc[3]) {
     if (!hit) {
@@ -1039,7 +1077,7 @@ __device__ __forceinline__ bool shade(const SceneView& S, const CamView& C, Path
     }
     double p[3], n[3];
     bool front;
-    const uint32_t mi = hit_record(S, ref, P.o, P.d, t, p, n, front);
+    const uint32_t mi = hit_record<LS>(S, ref, P.o, P.d, t, p, n, front);
     const DevMaterial& M = S.mats[mi];
     const uint32_t kind = M.kind;
     const bool lam = kind == CRT_LAMBERTIAN, met = kind == CRT_METAL, die = kind == CRT_DIELECTRIC;
@@ -1177,6 +1215,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LSCENE ?
         stage_lds(smem, Sg.fnodes, W.bytes_nodes);
         stage_lds(smem + W.lds_quads, Sg.quads, W.bytes_quads);
         S.quads = reinterpret_cast<const DevQuad*>(smem + W.lds_quads);
+        S.quads_lds = W.lds_quads;
+        S.refs_lds = W.lds_refs;
+        S.spheres_lds = W.spheres_f32 ? ~0u : W.lds_spheres;
         if (W.spheres_f32) {
             // sphere-only: the filter's pair records in LDS; refs are unused (slot = sphere),
             // and the f64 spheres (candidates' exact tests, shading) stay in HBM / L1
@@ -1326,7 +1367,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LSCENE ?
         if (COUNT) cs -= static_cast<uint32_t>(wall_clock64());
         if (R.state == kDone) {
             if (COUNT && wave_leader()) ctr.it_shade++;
-            bool ended = shade(S, CL, P, R.found, R.ref, R.tmax, acc);
+            bool ended = shade<LSCENE>(S, CL, P, R.found, R.ref, R.tmax, acc);
             // a scattered ray with no bounce left returns RGB::zero() (camera.h:211-213)
             if (!ended && P.depth == 0) ended = true;
             if (!ended) {
@@ -1460,7 +1501,7 @@ __global__ __launch_bounds__(kBlock) void hits_kernel(SceneView S, const double*
     if (trace<uint32_t, false>(S, st, o, d, t_min, tmax, ref, ctr)) {
         double p[3], nrm[3];
         bool front;
-        h.material = hit_record(S, ref, o, d, tmax, p, nrm, front);
+        h.material = hit_record<false>(S, ref, o, d, tmax, p, nrm, front);
         h.t = tmax;
         for (int k = 0; k < 3; ++k) { h.point[k] = p[k]; h.normal[k] = nrm[k]; }
         h.front_face = front ? 1 : 0;
