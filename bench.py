@@ -41,6 +41,16 @@ SCENE_DATA = {
 }
 
 
+def kernel_source_sha() -> str:
+    """Hash of the kernel sources: a PMC summary (profiles/pmc_latest.json) is used for
+    roofline.traffic only when it was collected on this exact kernel."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in ("crt_device.hip", "crt_internal.h"):
+        h.update((ROOT / "cpp_raytracer_amd" / "csrc" / f).read_bytes())
+    return h.hexdigest()[:16]
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -197,13 +207,19 @@ def main():
     rays_per_sample = cnt.rays / max(1, cnt.samples)
     flops = cnt.nodes_visited * 12 + cnt.sphere_tests * 23 + cnt.parallelogram_tests * 40 + cnt.rays * 50
     achieved_gbs = alg_bytes / (kernel_ms * 1e-3) / 1e9
-    traffic = None
+    workload = f"{args.scene} seed {args.seed}, {w}x{h}, {args.spp} spp, max_depth {args.depth}"
+    if (args.scene, w, h, args.spp, args.depth) == ("rtow_final", 1200, 800, 500, 50):
+        workload += " (BASELINE config 2)"
+    # HBM bytes per launch from the rocprofv3 PMC passes (FETCH_SIZE x2 + WRITE_SIZE, the guide's
+    # gfx950 correction; tools/gpu_pmc.sh + tools/pmc_summary.py) of this workload on this kernel
+    traffic, traffic_src = None, None
     pmc = Path(args.pmc_json)
-    if pmc.exists():
+    if pmc.exists() and world == 1:
         try:
             pj = json.loads(pmc.read_text())
-            if pj.get("workload") == f"{args.scene}:{w}x{h}x{args.spp}:d{args.depth}:n{world}":
+            if pj.get("workload") == workload and pj.get("kernel_source_sha") == kernel_source_sha():
                 traffic = pj.get("hbm_bytes_per_launch")
+                traffic_src = str(pmc.relative_to(ROOT)) if pmc.is_relative_to(ROOT) else str(pmc)
         except Exception:
             traffic = None
 
@@ -225,15 +241,13 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": SCENE_DATA.get(args.scene, f"synthetic: {args.scene} scene of the reference's src/main.cpp"),
-            "config": {"workload": f"{args.scene} seed {args.seed}, {w}x{h}, {args.spp} spp, max_depth {args.depth}"
-                                   f" (BASELINE config 2)" if (args.scene, w, h, args.spp, args.depth) ==
-                                   ("rtow_final", 1200, 800, 500, 50) else
-                                   f"{args.scene} seed {args.seed}, {w}x{h}, {args.spp} spp, max_depth {args.depth}",
+            "config": {"workload": workload,
                        "samples_per_step": h * w * args.spp, "primitives": int(info.num_primitives),
                        "bvh_nodes": int(info.num_nodes), "partition": f"{rb}-row blocks over {world} ranks, "
                        "RCCL all-gather of tiles overlapped with the next frame" if distributed else "whole frame on one GPU"},
             "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved_gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "traffic_source": traffic_src,
                          "kernel_ms": round(kernel_ms, 3),
                          "alg_bytes_per_launch": int(alg_bytes),
                          "basis": "SURVEY 8d algorithmic bytes (56 B/node, 36 B/sphere test, 124 B/quad test, "

@@ -77,7 +77,12 @@ struct CamView {
 struct Work {
     uint32_t owned_rows;   // rows of this tiling
     uint32_t row_block, tile_count, tile_index;
-    uint32_t tiles_x, tiles_y, tiles;  // 8x8 pixel tiles over (owned rows x width)
+    // one launch renders a band of the owned frame: owned rows [k0, k0 + bh) x columns
+    // [col0, col0 + bw), in kTileW x kTileH pixel tiles (launch_render: a band has at most 65535
+    // tiles either way, so a tile's coordinates pack into 16 bits each, and its partial sums
+    // stay within the partial-sum budget)
+    uint32_t col0, k0, bw, bh;
+    uint32_t tiles_x, tiles_y, tiles;
     uint32_t chunks, chunk_len;        // sample chunks per pixel
     // work queue, taken in order by the waves of a persistent grid (render_kernel): bulk items
     // (tile i / groups, chunks [(i % groups) * item_chunks, + item_chunks)), then tail items
@@ -108,13 +113,14 @@ struct Counters {
     unsigned long long cand, it_cand;        // two-pass leaves: exact tests of candidates (lanes / wave iterations)
 };
 
-// one lane's counts in the instrumented pass (32-bit: a lane handles one sample chunk), added to
-// the 64-bit Counters at the end
+// one lane's counts in the instrumented pass, added to the Counters when the lane ends; 64-bit:
+// a lane of the persistent grid traces units for the whole launch (a one-block grid on a large
+// frame would wrap 32-bit counts)
 struct LaneCounters {
-    uint32_t rays, nodes, sphere_tests, quad_tests;
-    uint32_t it_walk, it_leaf, it_shade;
-    uint32_t slow_nodes, it_slow;
-    uint32_t cand, it_cand;
+    unsigned long long rays, nodes, sphere_tests, quad_tests;
+    unsigned long long it_walk, it_leaf, it_shade;
+    unsigned long long slow_nodes, it_slow;
+    unsigned long long cand, it_cand;
 };
 
 // counts one per wave: only the lowest active lane increments
@@ -1310,15 +1316,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LSCENE ?
                 const uint32_t uu = item_pos + r, pix = uu & 63, chunk = item_chunk + (uu >> 6);
                 u_txy = item_txy;
                 u_cp = (chunk << 6) | pix;
+                // band-local column and owned row
                 const uint32_t col = (item_txy & 0xffffu) * kTileW + pix % kTileW, k = (item_txy >> 16) * kTileH + pix / kTileW;
-                if (chunk < W.chunks && col < C.w && k < W.owned_rows) {
+                if (chunk < W.chunks && col < W.bw && k < W.bh) {
                     s = chunk * W.chunk_len;
                     if (C.max_depth > 0) {
                         need = false;
                         start = true;
                     } else if (!COUNT) {
-                        double* dst = partial + (static_cast<size_t>(chunk) * W.owned_rows * C.w +
-                                                 static_cast<size_t>(k) * C.w + col) * 3;
+                        double* dst = partial + (static_cast<size_t>(chunk) * W.bh * W.bw +
+                                                 static_cast<size_t>(k) * W.bw + col) * 3;
                         dst[0] = 0;
                         dst[1] = 0;
                         dst[2] = 0;
@@ -1329,8 +1336,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LSCENE ?
         }
         if (start) {
             const uint32_t pix = u_cp & 63;
-            const uint32_t col = (u_txy & 0xffffu) * kTileW + pix % kTileW;
-            const uint32_t row = owned_row(W, (u_txy >> 16) * kTileH + pix / kTileW);
+            const uint32_t col = W.col0 + (u_txy & 0xffffu) * kTileW + pix % kTileW;
+            const uint32_t row = owned_row(W, W.k0 + (u_txy >> 16) * kTileH + pix / kTileW);
             start_path(CL, row, col, sample_seed(C.base_seed, row * C.w + col, s), P);
         }
         // one traversal set-up for new samples and scattered rays alike (the wave runs it once);
@@ -1380,8 +1387,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LSCENE ?
                     if (!COUNT) {
                         const uint32_t pix = u_cp & 63;
                         const uint32_t col = (u_txy & 0xffffu) * kTileW + pix % kTileW, k = (u_txy >> 16) * kTileH + pix / kTileW;
-                        double* dst = partial + (static_cast<size_t>(chunk) * W.owned_rows * C.w +
-                                                 static_cast<size_t>(k) * C.w + col) * 3;
+                        double* dst = partial + (static_cast<size_t>(chunk) * W.bh * W.bw +
+                                                 static_cast<size_t>(k) * W.bw + col) * 3;
                         dst[0] = acc[0];
                         dst[1] = acc[1];
                         dst[2] = acc[2];
@@ -1422,16 +1429,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LSCENE ?
 }
 
 // pixel_color /= spp (camera.h:290, rgb.h:76): sum the chunks in order, multiply by 1/spp.
+// One thread per pixel of the launch's band.
 __global__ __launch_bounds__(256) void resolve_kernel(const double* __restrict__ partial,
                                                       double* __restrict__ out, Work W, uint32_t w,
                                                       uint32_t h, double inv_spp) {
     const uint64_t i = static_cast<uint64_t>(blockIdx.x) * 256 + threadIdx.x;
-    const uint64_t owned = static_cast<uint64_t>(W.owned_rows) * w;
-    if (i >= owned) return;
-    const uint32_t k = static_cast<uint32_t>(i / w), col = static_cast<uint32_t>(i % w);
+    const uint64_t band = static_cast<uint64_t>(W.bh) * W.bw;
+    if (i >= band) return;
+    const uint32_t k = W.k0 + static_cast<uint32_t>(i / W.bw), col = W.col0 + static_cast<uint32_t>(i % W.bw);
     const uint32_t row = owned_row(W, k);
     const size_t pix = static_cast<size_t>(row) * w + col;
-    const size_t plane = owned * 3;
+    const size_t plane = band * 3;
     double r = partial[i * 3 + 0], g = partial[i * 3 + 1], b = partial[i * 3 + 2];
     for (uint32_t c = 1; c < W.chunks; ++c) {
         r = r + partial[c * plane + i * 3 + 0];
@@ -1708,6 +1716,15 @@ static size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
 constexpr size_t kLdsSceneBudget = CRT_LDS_BUDGET_KB * 1024;  // scene + stack per block
 constexpr size_t kLdsStackBudget = 32 * 1024 * dev::kBlock / 256;
 
+// Partial-sum budget per launch (bytes): the owned frame is rendered in bands whose partial sums
+// fit it (CRT_PARTIAL_MB overrides; tests force many small bands). 4 GiB holds a whole config-2
+// frame (2.9 GB) in one band; config 5 on one GPU (37.6 GB of partial sums) takes 10.
+static size_t partial_budget() {
+    if (const char* e = std::getenv("CRT_PARTIAL_MB"))
+        return static_cast<size_t>(std::max(1, std::atoi(e))) << 20;
+    return size_t{4} << 30;
+}
+
 template <typename SE, bool GSTACK, bool LSCENE>
 static int launch_render(const crt_scene* s, int device, const crt_camera* cam, const dev::Work& w0,
                          size_t lds, double* d_rgb, hipStream_t stream, crt_render_stats* count_stats) {
@@ -1717,11 +1734,11 @@ static int launch_render(const crt_scene* s, int device, const crt_camera* cam, 
     lds = W.lds_cam + align16(sizeof(dev::CamView));
     const uint64_t pixels = static_cast<uint64_t>(W.owned_rows) * cam->image_w;
     // Sample chunks: a function of spp ONLY, so every pixel's sum is grouped identically whatever
-    // the tiling / number of GPUs / lane schedule (bit-identical frames for 1..N devices): 4
-    // samples, or spp / 192 above 768 spp. A unit is the grain the grid drains on: per-rank share
-    // at 8 GPUs 12.2 ms with 4-sample chunks vs 13.0 with 8 (one GPU 87.4 vs 87.5; the partial
-    // sums double to 2.9 GB per config-2 frame). The persistent grid's waves take (tile, chunk) items
-    // from a queue in tile-major order (render_kernel).
+    // the tiling / number of GPUs / lane schedule / band split (bit-identical frames for 1..N
+    // devices): 4 samples, or spp / 192 above 768 spp. A unit is the grain the grid drains on:
+    // per-rank share at 8 GPUs 12.2 ms with 4-sample chunks vs 13.0 with 8 (one GPU 87.4 vs 87.5;
+    // the partial sums double to 2.9 GB per config-2 frame). The persistent grid's waves take
+    // (tile, chunk) items from a queue in tile-major order (render_kernel).
     const uint32_t spp = cam->samples_per_pixel;
 #ifndef CRT_CHUNK_MIN
 #define CRT_CHUNK_MIN 4
@@ -1731,49 +1748,41 @@ static int launch_render(const crt_scene* s, int device, const crt_camera* cam, 
     W.rb_shift = 32;
     for (uint32_t sh = 0; sh < 31; ++sh)
         if ((1u << sh) == W.row_block) W.rb_shift = sh;
-    // the grid: every resident block (more would only wait), fewer when the items are fewer
+    // Bands: rectangles of bx x by tiles over the owned rows x width, each one launch (render +
+    // resolve). bx, by <= 65535 (a unit packs its tile as tx | ty << 16), and a band's partial
+    // sums (64 pixels x 3 x chunks doubles per tile) fit the budget. A pixel's chunks are summed
+    // in the same order in any band, so the split does not change frames.
+    constexpr uint64_t kMaxTiles = 65535;
+    const uint64_t tiles_x_all = (static_cast<uint64_t>(cam->image_w) + dev::kTileW - 1) / dev::kTileW;
+    const uint64_t tiles_y_all = (static_cast<uint64_t>(W.owned_rows) + dev::kTileH - 1) / dev::kTileH;
+    const uint64_t tile_bytes = 64ull * 3 * sizeof(double) * W.chunks;
+    const uint64_t cap = std::max<uint64_t>(1, partial_budget() / tile_bytes);
+    const uint32_t bx = static_cast<uint32_t>(std::min({tiles_x_all, kMaxTiles, cap}));
+    const uint32_t by = static_cast<uint32_t>(std::min({tiles_y_all, kMaxTiles, std::max<uint64_t>(1, cap / bx)}));
+    // the grid: every resident block (more would only wait), fewer when a band's items are fewer
     int cus = 0, per_cu = 0;
     HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
     HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(
         &per_cu, reinterpret_cast<const void*>(dev::render_kernel<SE, GSTACK, LSCENE, false>), dev::kBlock, lds));
     constexpr uint32_t kWavesPerBlock = dev::kBlock / 64;
-    uint64_t blocks = std::max<uint64_t>(1, std::min<uint64_t>(static_cast<uint64_t>(std::max(1, cus)) * std::max(1, per_cu),
-                                                               (static_cast<uint64_t>(W.tiles) * W.chunks + kWavesPerBlock - 1) / kWavesPerBlock));
+    uint64_t resident = static_cast<uint64_t>(std::max(1, cus)) * std::max(1, per_cu);
     if (const char* e = std::getenv("CRT_GRID_BLOCKS"))  // schedule tests: a smaller grid, same frame
-        blocks = std::max<uint64_t>(1, std::min<uint64_t>(blocks, static_cast<uint64_t>(std::max(1, std::atoi(e)))));
-    // Items: bulk items of K chunks for the first 8/9 of each tile's chunks, then the rest in
-    // one-chunk items at the end of the queue (CRT_TAIL_CHUNKS), so the grid drains on small
-    // items; a wave's lanes cross from item to item without waiting either way. K keeps an item
-    // small against a wave's share of the frame (a tile costs up to ~10x another): a 30th of
-    // the units per lane, at most 7 (config 2: 7 on one GPU, 3/1/1 for a rank's share at 2/4/8
-    // GPUs; no tail items with K = 1). Measured on config 2, one GPU (Msamples/s): K = 1 5127,
-    // 7 5273, 14 4828, 28 4025; a rank's share at 4 / 8 GPUs took 24.8 / 14.1 ms with K = 1,
-    // 26.1 / 19.4 with K = 2 / 7 (CRT_ITEM_CHUNKS, CRT_TAIL_CHUNKS override).
+        resident = std::max<uint64_t>(1, std::min<uint64_t>(resident, static_cast<uint64_t>(std::max(1, std::atoi(e)))));
     auto knob = [](const char* name, uint32_t dflt) {
         const char* e = std::getenv(name);
         return e ? static_cast<uint32_t>(std::max(0, std::min(4096, std::atoi(e)))) : dflt;
     };
-    const uint64_t per_lane = static_cast<uint64_t>(W.tiles) * W.chunks / (blocks * kWavesPerBlock);
-    W.item_chunks = std::max<uint32_t>(1, knob("CRT_ITEM_CHUNKS", static_cast<uint32_t>(std::min<uint64_t>(7, std::max<uint64_t>(1, per_lane / 30)))));
-    const uint32_t tail_want = std::min(W.chunks, knob("CRT_TAIL_CHUNKS", W.item_chunks > 1 ? W.chunks / 9 : 0));
-    W.groups = (W.chunks - tail_want) / W.item_chunks;
-    W.bulk_chunks = W.groups * W.item_chunks;
-    W.tail_chunks = W.chunks - W.bulk_chunks;
-    const uint64_t bulk_items = static_cast<uint64_t>(W.tiles) * W.groups;
-    const uint64_t items = bulk_items + static_cast<uint64_t>(W.tiles) * W.tail_chunks;
-    if (items >= 0xffffffffull) return fail(CRT_E_INVALID, "frame too large for one launch");
-    W.n_items = static_cast<uint32_t>(items);
-    W.bulk_items = static_cast<uint32_t>(bulk_items);
-    const size_t plane = static_cast<size_t>(pixels) * 3;  // partials indexed by owned pixel
 
     double* partial = nullptr;
     SE* gstack = nullptr;
     dev::Counters* ctr = nullptr;
     const bool count = count_stats != nullptr;
+    const uint64_t band_px = std::min<uint64_t>(static_cast<uint64_t>(bx) * dev::kTileW, cam->image_w) *
+                             std::min<uint64_t>(static_cast<uint64_t>(by) * dev::kTileH, W.owned_rows);
     if (!count)
-        HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&partial), plane * W.chunks * sizeof(double), stream));
+        HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&partial), band_px * 3 * W.chunks * sizeof(double), stream));
     if (GSTACK) {
-        size_t bytes = static_cast<size_t>(s->depth + 3) * blocks * dev::kBlock * sizeof(SE);  // + 2 guard levels
+        size_t bytes = static_cast<size_t>(s->depth + 3) * resident * dev::kBlock * sizeof(SE);  // + 2 guard levels
         HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&gstack), bytes, stream));
     }
     if (count) {
@@ -1782,7 +1791,6 @@ static int launch_render(const crt_scene* s, int device, const crt_camera* cam, 
     }
     uint32_t* queue = nullptr;
     HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&queue), 256, stream));
-    HIP_TRY(hipMemsetAsync(queue, 0, sizeof(uint32_t), stream));
     W.queue = queue;
     dev::SceneView S = view_of(c);
     dev::CamView C = cam_view(cam);
@@ -1791,21 +1799,55 @@ static int launch_render(const crt_scene* s, int device, const crt_camera* cam, 
         HIP_TRY(hipEventCreate(&e0));
         HIP_TRY(hipEventCreate(&e1));
         HIP_TRY(hipEventRecord(e0, stream));
-        hipLaunchKernelGGL((dev::render_kernel<SE, GSTACK, LSCENE, true>), dim3(static_cast<uint32_t>(blocks)),
-                           dim3(dev::kBlock), lds, stream, S, C, W, partial, gstack, ctr);
-        HIP_TRY(hipGetLastError());
-        HIP_TRY(hipEventRecord(e1, stream));
-    } else {
-        hipLaunchKernelGGL((dev::render_kernel<SE, GSTACK, LSCENE, false>), dim3(static_cast<uint32_t>(blocks)),
-                           dim3(dev::kBlock), lds, stream, S, C, W, partial, gstack, ctr);
-        HIP_TRY(hipGetLastError());
-        const uint32_t rb = static_cast<uint32_t>((pixels + 255) / 256);
-        if (rb) {
-            hipLaunchKernelGGL(dev::resolve_kernel, dim3(rb), dim3(256), 0, stream, partial, d_rgb,
-                               W, cam->image_w, cam->image_h, C.inv_spp);
-            HIP_TRY(hipGetLastError());
+    }
+    for (uint64_t ty0 = 0; ty0 < tiles_y_all; ty0 += by) {
+        for (uint64_t tx0 = 0; tx0 < tiles_x_all; tx0 += bx) {
+            W.col0 = static_cast<uint32_t>(tx0 * dev::kTileW);
+            W.k0 = static_cast<uint32_t>(ty0 * dev::kTileH);
+            W.bw = static_cast<uint32_t>(std::min<uint64_t>(static_cast<uint64_t>(bx) * dev::kTileW, cam->image_w - W.col0));
+            W.bh = static_cast<uint32_t>(std::min<uint64_t>(static_cast<uint64_t>(by) * dev::kTileH, W.owned_rows - W.k0));
+            W.tiles_x = (W.bw + dev::kTileW - 1) / dev::kTileW;
+            W.tiles_y = (W.bh + dev::kTileH - 1) / dev::kTileH;
+            W.tiles = W.tiles_x * W.tiles_y;
+            const uint64_t blocks = std::max<uint64_t>(
+                1, std::min<uint64_t>(resident, (static_cast<uint64_t>(W.tiles) * W.chunks + kWavesPerBlock - 1) / kWavesPerBlock));
+            // Items: bulk items of K chunks for the first 8/9 of each tile's chunks, then the
+            // rest in one-chunk items at the end of the queue (CRT_TAIL_CHUNKS), so the grid
+            // drains on small items; a wave's lanes cross from item to item without waiting
+            // either way. K keeps an item small against a wave's share of the band (a tile costs
+            // up to ~10x another): a 30th of the units per lane, at most 7 (config 2: 7 on one
+            // GPU, 3/1/1 for a rank's share at 2/4/8 GPUs; no tail items with K = 1). Measured on
+            // config 2, one GPU (Msamples/s): K = 1 5127, 7 5273, 14 4828, 28 4025; a rank's
+            // share at 4 / 8 GPUs took 24.8 / 14.1 ms with K = 1, 26.1 / 19.4 with K = 2 / 7
+            // (CRT_ITEM_CHUNKS, CRT_TAIL_CHUNKS override).
+            const uint64_t per_lane = static_cast<uint64_t>(W.tiles) * W.chunks / (blocks * kWavesPerBlock);
+            W.item_chunks = std::max<uint32_t>(1, knob("CRT_ITEM_CHUNKS", static_cast<uint32_t>(std::min<uint64_t>(7, std::max<uint64_t>(1, per_lane / 30)))));
+            const uint32_t tail_want = std::min(W.chunks, knob("CRT_TAIL_CHUNKS", W.item_chunks > 1 ? W.chunks / 9 : 0));
+            W.groups = (W.chunks - tail_want) / W.item_chunks;
+            W.bulk_chunks = W.groups * W.item_chunks;
+            W.tail_chunks = W.chunks - W.bulk_chunks;
+            const uint64_t bulk_items = static_cast<uint64_t>(W.tiles) * W.groups;
+            const uint64_t items = bulk_items + static_cast<uint64_t>(W.tiles) * W.tail_chunks;
+            if (items >= 0xffffffffull) return fail(CRT_E_INVALID, "band too large for one launch");
+            W.n_items = static_cast<uint32_t>(items);
+            W.bulk_items = static_cast<uint32_t>(bulk_items);
+            HIP_TRY(hipMemsetAsync(queue, 0, sizeof(uint32_t), stream));
+            if (count) {
+                hipLaunchKernelGGL((dev::render_kernel<SE, GSTACK, LSCENE, true>), dim3(static_cast<uint32_t>(blocks)),
+                                   dim3(dev::kBlock), lds, stream, S, C, W, partial, gstack, ctr);
+                HIP_TRY(hipGetLastError());
+            } else {
+                hipLaunchKernelGGL((dev::render_kernel<SE, GSTACK, LSCENE, false>), dim3(static_cast<uint32_t>(blocks)),
+                                   dim3(dev::kBlock), lds, stream, S, C, W, partial, gstack, ctr);
+                HIP_TRY(hipGetLastError());
+                const uint64_t rb = (static_cast<uint64_t>(W.bw) * W.bh + 255) / 256;
+                hipLaunchKernelGGL(dev::resolve_kernel, dim3(static_cast<uint32_t>(rb)), dim3(256), 0, stream, partial,
+                                   d_rgb, W, cam->image_w, cam->image_h, C.inv_spp);
+                HIP_TRY(hipGetLastError());
+            }
         }
     }
+    if (count) HIP_TRY(hipEventRecord(e1, stream));
     if (partial) HIP_TRY(hipFreeAsync(partial, stream));
     HIP_TRY(hipFreeAsync(queue, stream));
     if (gstack) HIP_TRY(hipFreeAsync(gstack, stream));
@@ -1933,9 +1975,6 @@ int device_render(const crt_scene* s, int device, const crt_camera* cam, const c
         }
         return CRT_OK;
     }
-    W.tiles_x = (cam->image_w + dev::kTileW - 1) / dev::kTileW;
-    W.tiles_y = (W.owned_rows + dev::kTileH - 1) / dev::kTileH;
-    W.tiles = W.tiles_x * W.tiles_y;
     W.sphere_only = (s->quads.empty() && !s->spheres.empty()) ? 1u : 0u;
     W.spheres_f32 = (W.sphere_only && s->dev[device].spheres_f32_ok) ? 1u : 0u;
     W.exact_slab = (s->exact_slab || std::getenv("CRT_EXACT_SLAB") != nullptr) ? 1u : 0u;

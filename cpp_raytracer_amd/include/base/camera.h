@@ -53,11 +53,20 @@ class Camera {
     void init() {
         if (camera_lookat) camera.dir = *camera_lookat - camera.origin;
         if (!focus_dist) focus_dist = camera.dir.mag();
+        // the ABI carries these as 32-bit counts: refuse values a cast would truncate
+        const auto u32 = [](size_t x, const char* what) {
+            if (x > UINT32_MAX) {
+                std::cout << "Error: Camera: " << what << " = " << x
+                          << " exceeds the render path's 32-bit range (4294967295)" << std::endl;
+                std::exit(-1);
+            }
+            return static_cast<uint32_t>(x);
+        };
         crt_camera_settings s{};
-        s.image_w = static_cast<uint32_t>(image_w);
-        s.image_h = static_cast<uint32_t>(image_h);
-        s.samples_per_pixel = static_cast<uint32_t>(samples_per_pixel);
-        s.max_depth = static_cast<uint32_t>(max_depth);
+        s.image_w = u32(image_w, "image width");
+        s.image_h = u32(image_h, "image height");
+        s.samples_per_pixel = u32(samples_per_pixel, "samples_per_pixel");
+        s.max_depth = u32(max_depth, "max_depth");
         put(s.center, camera.origin);
         put(s.direction, camera.dir);
         put(s.up, view_up_dir);

@@ -1,8 +1,8 @@
 """Row-tile partition of a frame over ranks and the tile gather (RCCL over xGMI on MI355X; any
 torch.distributed backend works, gloo in the CPU tests).
 
-Rows are dealt in blocks of `row_block` (default 16): row r belongs to rank (r // row_block) %
-world. Interleaving balances the >10x per-row cost variance of real scenes (the sky rows of
+Rows are dealt in blocks of `row_block` (default 4, the block crt_render and bench.py use): row r
+belongs to rank (r // row_block) % world. Interleaving balances the >10x per-row cost variance of real scenes (the sky rows of
 RTOW cost almost nothing). Every rank renders only its rows (crt_render_async with
 crt_tiling{row_block, world, rank}); the frame is then assembled from equal-size padded tiles with
 one all-gather. Because the RNG is per (pixel, sample) and the sample-chunk grouping depends only on
@@ -22,7 +22,7 @@ def owned_rows(height: int, row_block: int, world: int, rank: int) -> list[int]:
 class TileGather:
     """Gathers every rank's rows of a (h, w, 3) frame into a full frame on every rank."""
 
-    def __init__(self, height: int, width: int, world: int, rank: int, device, row_block: int = 16,
+    def __init__(self, height: int, width: int, world: int, rank: int, device, row_block: int = 4,
                  dtype=torch.float64, group=None):
         self.h, self.w, self.world, self.rank, self.group = height, width, world, rank, group
         rows = [owned_rows(height, row_block, world, k) for k in range(world)]

@@ -224,7 +224,8 @@ int crt_render_count(const crt_scene* scene, int device, const crt_camera* cam,
                      const crt_tiling* tiling, crt_render_stats* stats);
 
 /* Blocking whole-frame render over devices [0, num_devices): rows are dealt to devices in
- * blocks of 16, rendered concurrently, and gathered into HOST memory h_rgb. */
+ * blocks of 4 (crt_tiling{4, num_devices, d}), rendered concurrently, and gathered into HOST
+ * memory h_rgb. */
 int crt_render(crt_scene* scene, const crt_camera* cam, int num_devices, double* h_rgb,
                crt_render_stats* stats);
 

@@ -7,12 +7,18 @@ counter group ran in its own rocprofv3 --pmc pass. Values are averaged over the 
 the product render kernel (the non-instrumented variant: template COUNT = false).
 
 usage: python tools/pmc_summary.py <pmc dir> <workload key> <out.json>
+The workload key is bench.py's config.workload string; the summary also records the hash of the
+kernel sources (bench.kernel_source_sha), so bench.py only reports `traffic` measured on the
+kernel it is timing.
 """
 import csv
 import json
 import sys
 from collections import defaultdict
 from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+from bench import kernel_source_sha  # noqa: E402
 
 KERNEL = "crt::dev::render_kernel<unsigned short, false, true, false>"
 
@@ -27,7 +33,8 @@ def main():
     if not vals:
         raise SystemExit(f"no {KERNEL} rows under {src}")
     avg = {k: sum(v) / len(v) for k, v in vals.items()}
-    res = {"workload": workload, "kernel": KERNEL, "launches": {k: len(v) for k, v in vals.items()}}
+    res = {"workload": workload, "kernel": KERNEL, "kernel_source_sha": kernel_source_sha(),
+           "launches": {k: len(v) for k, v in vals.items()}}
     res.update({k: avg[k] for k in sorted(avg)})
     if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
         res["FETCH_SIZE_KB"] = avg["FETCH_SIZE"]
