@@ -9,6 +9,8 @@
 // sample's colour by a few ulps and never changes a path.
 #include <hip/hip_runtime.h>
 
+#define CRT_HD __host__ __device__ __forceinline__
+
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
@@ -60,6 +62,8 @@ struct SceneView {
     const DevQuad* quads;
     const uint32_t* quad_mat;
     const DevMaterial* mats;
+    const DevQuadF* quadf;       // f32 filter records of the parallelograms (HBM)
+    uint32_t quadf_lds;          // LSCENE kernels: LDS byte offset of the staged copy
     // LSCENE kernels: LDS byte offsets of the staged refs / f64 spheres / parallelograms, read
     // through typed LDS pointers (ds_read, not flat); spheres_lds = ~0u when the spheres stay in HBM
     uint32_t refs_lds, spheres_lds, quads_lds;
@@ -92,8 +96,8 @@ struct Work {
     uint32_t item_chunks, groups, bulk_chunks, tail_chunks;
     uint32_t rb_shift;      // log2(row_block) when it is a power of two, else 32
     // LDS layout of the scene-staging kernels (byte offsets / 16-byte padded sizes)
-    uint32_t lds_nodes, lds_refs, lds_spheres, lds_quads, lds_stack;
-    uint32_t bytes_nodes, bytes_refs, bytes_spheres, bytes_quads;
+    uint32_t lds_nodes, lds_refs, lds_spheres, lds_quads, lds_quadf, lds_stack;
+    uint32_t bytes_nodes, bytes_refs, bytes_spheres, bytes_quads, bytes_quadf;
     uint32_t sphere_only;   // every primitive is a sphere: refs[slot] == slot
     uint32_t exact_slab;    // the scene needs walk_step's EXACT variant for every ray
     uint32_t ntop;          // HBM-scene kernels: f32 nodes [0, ntop) bytes staged in LDS at offset 0
@@ -101,6 +105,7 @@ struct Work {
     uint32_t lds_cam;       // LDS copy of the CamView (read where used: keeps it out of SGPRs)
     uint32_t f32_ok;        // node bounds fit the f32 walk's error analysis (else f64 decides)
     uint32_t spheres_f32;   // sphere-only scene within the f32 filter's range (two-pass leaves)
+    uint32_t quads_f32;     // parallelogram-only scene within its f32 filter's range (two-pass leaves)
     float tmin32;           // RN32(camera t_min)
 };
 
@@ -445,6 +450,16 @@ __device__ __forceinline__ DevSphere sphere_global(const DevSphere* p) {
     const Dvec2 a = q->a, b = q->b;
     DevSphere r;
     r.c[0] = a.x; r.c[1] = a.y; r.c[2] = b.x; r.r = b.y;
+    return r;
+}
+// an f32 parallelogram record in HBM through a typed global pointer (4 x 16-byte loads)
+typedef __attribute__((address_space(1))) const Fvec4 GlobalFvec4;
+__device__ __forceinline__ DevQuadF quadf_global(const DevQuadF* p) {
+    const GlobalFvec4* q = (GlobalFvec4*)p;
+    DevQuadF r;
+    Fvec4* dst = reinterpret_cast<Fvec4*>(&r);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) dst[k] = q[k];
     return r;
 }
 // a 16-byte aligned record (DevSphere, DevQuad, u32) at an LDS byte offset, read as ds_read
@@ -920,7 +935,7 @@ __device__ __forceinline__ void walk(const SceneView& S, Stack<SE>& st, const do
 template <typename SE, bool COUNT, bool TOP, bool LS>
 __device__ __forceinline__ void leaf_step(const SceneView& S, Stack<SE>& st, const double o[3],
                                           const double d[3], double tmin, bool sphere_only, bool pairs,
-                                          Trav& R, LaneCounters& ctr) {
+                                          bool qfilter, Trav& R, LaneCounters& ctr) {
     const uint2 range = make_uint2(R.first, R.count);  // index, count
     const uint32_t end = range.x + range.y;
     const double ia = recip_a(R.a), lo = lim_tmin(tmin, R.a);
@@ -964,6 +979,38 @@ __device__ __forceinline__ void leaf_step(const SceneView& S, Stack<SE>& st, con
                 R.tmax32 = tmax_f32(t);
                 hi = lim_tmax(t, R.a);
                 R.ref = i;
+                R.found = true;
+            }
+        }
+    } else if (qfilter && range.y <= 32 && quad_ray32_ok(o, d)) {
+        // parallelogram-only scenes (a slot is its parallelogram's index): the same two passes,
+        // with the f32 filter of crt_quad_filter.h (quad_candidate) in pass 1
+        QuadRay32 L;
+        quad_ray32(o, d, tmin, R.tmax, L);
+        uint32_t cand = 0;
+        for (uint32_t i = 0; i < range.y; ++i) {
+            if (COUNT) {
+                ctr.quad_tests++;
+                if (wave_leader()) ctr.it_leaf++;
+            }
+            const DevQuadF q = LS ? lds_rec<DevQuadF>(S.quadf_lds + ((range.x + i) << 6)) : quadf_global(S.quadf + range.x + i);
+            cand |= static_cast<uint32_t>(quad_candidate(q, L, [](float x) { return __builtin_amdgcn_rcpf(x); })) << i;
+        }
+        while (cand) {
+            if (COUNT) {
+                ctr.cand++;
+                if (wave_leader()) ctr.it_cand++;
+            }
+            const uint32_t i = range.x + static_cast<uint32_t>(__builtin_ctz(cand));
+            cand &= cand - 1;
+            double t;
+            bool h;
+            if constexpr (LS) h = hit_quad(lds_rec<DevQuad>(S.quads_lds + (i << 7)), o, d, tmin, R.tmax, t);
+            else h = hit_quad(S.quads[i], o, d, tmin, R.tmax, t);
+            if (h) {
+                R.tmax = t;
+                R.tmax32 = tmax_f32(t);
+                R.ref = kRefQuad | i;
                 R.found = true;
             }
         }
@@ -1222,6 +1269,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LSCENE ?
         stage_lds(smem + W.lds_quads, Sg.quads, W.bytes_quads);
         S.quads = reinterpret_cast<const DevQuad*>(smem + W.lds_quads);
         S.quads_lds = W.lds_quads;
+        if (W.quads_f32) {  // the parallelogram filter's records
+            stage_lds(smem + W.lds_quadf, Sg.quadf, W.bytes_quadf);
+            S.quadf_lds = W.lds_quadf;
+        }
         S.refs_lds = W.lds_refs;
         S.spheres_lds = W.spheres_f32 ? ~0u : W.lds_spheres;
         if (W.spheres_f32) {
@@ -1361,7 +1412,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LSCENE ?
             }
             if (COUNT) cw += static_cast<uint32_t>(wall_clock64());
             if (COUNT) cl -= static_cast<uint32_t>(wall_clock64());
-            if (R.state == kLeaf) leaf_step<SE, COUNT, kTopTreelet && !LSCENE, LSCENE>(S, st, P.o, P.d, C.t_min, W.sphere_only != 0, W.spheres_f32 != 0, R, ctr);
+            if (R.state == kLeaf) leaf_step<SE, COUNT, kTopTreelet && !LSCENE, LSCENE>(S, st, P.o, P.d, C.t_min, W.sphere_only != 0, W.spheres_f32 != 0, W.quads_f32 != 0, R, ctr);
             if (COUNT) cl += static_cast<uint32_t>(wall_clock64());
             const uint64_t pending = __ballot(R.state == kWalk);
             const uint64_t finished = __ballot(R.state == kDone);
@@ -1526,7 +1577,8 @@ __global__ __launch_bounds__(kBlock) void hits_kernel(SceneView S, const double*
 // host launch plumbing
 
 static dev::SceneView view_of(const DeviceCopy& c) {
-    return dev::SceneView{c.nodes, c.fnodes, 0, c.refs, c.spheres, c.spair, 0, c.sphere_mat, c.quads, c.quad_mat, c.mats};
+    return dev::SceneView{c.nodes, c.fnodes, 0, c.refs, c.spheres, c.spair, 0, c.sphere_mat, c.quads, c.quad_mat,
+                          c.mats, c.quadf, 0};
 }
 
 int device_count(int* n) {
@@ -1623,12 +1675,38 @@ int device_upload(crt_scene* s, int device) {
         DevSpherePair& last = spair[n_sp - 1];
         last.cx[1] = last.cy[1] = last.cz[1] = last.r2e[1] = 0;
     }
+    // parallelogram filter records (crt_quad_filter.h): f32 v, s1, s2, sn and rounded-up norms
+    std::vector<DevQuadF> quadf(n_q);
+    bool quads_f32_ok = true;
+    for (size_t i = 0; i < n_q; ++i) {
+        const DevQuad& q = s->quads[i];
+        DevQuadF& f = quadf[i];
+        double sn1 = 0, S1 = 0, S2 = 0;
+        for (int k = 0; k < 3; ++k) {
+            f.v[k] = static_cast<float>(q.v[k]);
+            f.s1[k] = static_cast<float>(q.s1[k]);
+            f.s2[k] = static_cast<float>(q.s2[k]);
+            f.sn[k] = static_cast<float>(q.sn[k]);
+            sn1 += std::fabs(q.sn[k]);
+            S1 += std::fabs(q.s1[k]);
+            S2 += std::fabs(q.s2[k]);
+            if (!(std::fabs(q.v[k]) <= kF32QuadMax && std::fabs(q.s1[k]) <= kF32QuadMax &&
+                  std::fabs(q.s2[k]) <= kF32QuadMax))
+                quads_f32_ok = false;
+        }
+        if (!(sn1 >= 0x1p-64 && sn1 <= 0x1p40)) quads_f32_ok = false;
+        f.sn1 = f32_up(sn1 * (1 + 0x1p-20));
+        f.ka = f32_up(sn1 * S2 * (1 + 0x1p-20));
+        f.kb = f32_up(sn1 * S1 * (1 + 0x1p-20));
+        f.pad = 0;
+    }
     size_t off_refs = align256(off_fnodes + n_nodes * sizeof(DevNodeF));
     size_t off_sp = align256(off_refs + n_refs * 4);
     size_t off_spp = align256(off_sp + n_sp * sizeof(DevSphere));
     size_t off_spm = align256(off_spp + n_sp * sizeof(DevSpherePair));
     size_t off_q = align256(off_spm + n_sp * 4);
-    size_t off_qm = align256(off_q + n_q * sizeof(DevQuad));
+    size_t off_qf = align256(off_q + n_q * sizeof(DevQuad));
+    size_t off_qm = align256(off_qf + n_q * sizeof(DevQuadF));
     size_t off_m = align256(off_qm + n_q * 4);
     size_t total = align256(off_m + std::max<size_t>(1, n_m) * sizeof(DevMaterial));
     void* base = nullptr;
@@ -1646,6 +1724,7 @@ int device_upload(crt_scene* s, int device) {
     if (e == hipSuccess) e = up(off_spp, spair.data(), n_sp * sizeof(DevSpherePair));
     if (e == hipSuccess) e = up(off_spm, s->sphere_mat.data(), n_sp * 4);
     if (e == hipSuccess) e = up(off_q, s->quads.data(), n_q * sizeof(DevQuad));
+    if (e == hipSuccess) e = up(off_qf, quadf.data(), n_q * sizeof(DevQuadF));
     if (e == hipSuccess) e = up(off_qm, s->quad_mat.data(), n_q * 4);
     if (e == hipSuccess) e = up(off_m, s->dmats.data(), n_m * sizeof(DevMaterial));
     if (e != hipSuccess) {
@@ -1663,6 +1742,8 @@ int device_upload(crt_scene* s, int device) {
     c.spheres_f32_ok = spheres_f32_ok && std::getenv("CRT_F64_SPHERES") == nullptr;
     c.sphere_mat = reinterpret_cast<uint32_t*>(b + off_spm);
     c.quads = reinterpret_cast<DevQuad*>(b + off_q);
+    c.quadf = reinterpret_cast<DevQuadF*>(b + off_qf);
+    c.quads_f32_ok = quads_f32_ok && std::getenv("CRT_F64_QUADS") == nullptr;
     c.quad_mat = reinterpret_cast<uint32_t*>(b + off_qm);
     c.mats = reinterpret_cast<DevMaterial*>(b + off_m);
     c.valid = true;
@@ -1900,7 +1981,9 @@ static int dispatch_render(const crt_scene* s, int device, const crt_camera* cam
     W.bytes_spheres = static_cast<uint32_t>(align16(s->spheres.size() * (W.spheres_f32 ? sizeof(DevSpherePair)
                                                                                          : sizeof(DevSphere))));
     W.bytes_quads = static_cast<uint32_t>(align16(s->quads.size() * sizeof(DevQuad)));
-    const size_t scene_bytes = static_cast<size_t>(W.bytes_nodes) + W.bytes_refs + W.bytes_spheres + W.bytes_quads;
+    W.bytes_quadf = W.quads_f32 ? static_cast<uint32_t>(s->quads.size() * sizeof(DevQuadF)) : 0u;
+    const size_t scene_bytes = static_cast<size_t>(W.bytes_nodes) + W.bytes_refs + W.bytes_spheres + W.bytes_quads +
+                               W.bytes_quadf;
     const uint32_t level = static_cast<uint32_t>(dev::kBlock * sizeof(SE));  // one stack level
     // the sentinel is the last node; refs are byte offsets into the f32 node array
     W.sentinel = static_cast<uint32_t>(s->dnodes.size() - 1) << kNodeFShift;
@@ -1915,6 +1998,7 @@ static int dispatch_render(const crt_scene* s, int device, const crt_camera* cam
         W.lds_refs = W.lds_nodes + W.bytes_nodes;
         W.lds_spheres = W.lds_refs + W.bytes_refs;
         W.lds_quads = W.lds_spheres + W.bytes_spheres;
+        W.lds_quadf = W.lds_quads + W.bytes_quads;
         W.lds_stack = stack_at(scene_bytes);
         return launch_render<SE, false, true>(s, device, cam, W, W.lds_stack + stack_bytes, d_rgb, st, count_stats);
     }
@@ -1977,6 +2061,7 @@ int device_render(const crt_scene* s, int device, const crt_camera* cam, const c
     }
     W.sphere_only = (s->quads.empty() && !s->spheres.empty()) ? 1u : 0u;
     W.spheres_f32 = (W.sphere_only && s->dev[device].spheres_f32_ok) ? 1u : 0u;
+    W.quads_f32 = (s->spheres.empty() && !s->quads.empty() && s->dev[device].quads_f32_ok) ? 1u : 0u;
     W.exact_slab = (s->exact_slab || std::getenv("CRT_EXACT_SLAB") != nullptr) ? 1u : 0u;
     hipStream_t st = static_cast<hipStream_t>(stream);
     if (count_stats) HIP_TRY(hipStreamCreate(&st));

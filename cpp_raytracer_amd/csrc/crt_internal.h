@@ -9,6 +9,7 @@
 #include <vector>
 
 #include "../../include/crt_render.h"
+#include "crt_quad_filter.h"
 
 namespace crt {
 
@@ -100,6 +101,8 @@ struct DeviceCopy {
     bool spheres_f32_ok = false;     // every sphere within +-kF32SphereMax
     uint32_t* sphere_mat = nullptr;
     DevQuad* quads = nullptr;
+    DevQuadF* quadf = nullptr;       // f32 filter records (crt_quad_filter.h)
+    bool quads_f32_ok = false;       // every parallelogram within the filter's range
     uint32_t* quad_mat = nullptr;
     DevMaterial* mats = nullptr;
     // per-device scratch reused across renders (partial sums of sample chunks)

@@ -1,0 +1,131 @@
+// The parallelogram candidate filter of the render kernel's two-pass leaves (crt_device.hip
+// leaf_step), shared with its host fuzzer (tools/fuzz_quad_filter.cpp), which runs this exact
+// f32 sequence against the exact test.
+//
+// The exact test is Parallelogram::hit_by (parallelogram.h:177-240) in f64:
+//   den = n.d; |den| < 1e-9 -> miss; t = n.(v - o) / den; !(tmin < t < tmax) -> miss;
+//   w = (o + d t) - v; alpha = sn.(w x s2), beta = sn.(s1 x w); hit iff alpha, beta in [0, 1]
+// (n = unit normal, sn = n / |n|^2 of the ctor, parallelogram.h:269-296). The filter returns false
+// only where that test provably misses, for this t_max and any smaller one: t <= t_min, t >= t_max,
+// alpha or beta outside [0, 1]. It computes the same quantities in f32 from f32-rounded inputs:
+//   num' = sn'.(v' - o'), den' = sn'.d', t' = num' * rcp(den')       (sn is parallel to n, so
+//   num'/den' estimates t; the |n| scale cancels)
+//   w' = d' t' - (v' - o'), alpha' = sn'.(w' x s2'), beta' = sn'.(s1' x w')
+// Error bounds, with u = 2^-24, V = max|v|, O = max|o|, D = max|d|, SN1 = |sn|_1, S1 = |s1|_1,
+// S2 = |s2|_1 (each input rounding, product and sum rounds once, fma once):
+//   |num' - num| <= a' = 6u SN1 (V + O),   |den' - den| <= b' = 5u SN1 D
+//   for |den'| > 2 b':   |num'/den' - t| <= 2 (a' + b' |num'/den'|) / |den'|
+//   rcp (1 ulp) and the product add 3.2u |t'|                      =>  Et
+//   |w'_k - w_k| <= D Et + 3u Mw,  Mw = O + D |t'| + V  (bounds |o|, |d t|, |v|, |w|)
+//   |alpha' - alpha| <= SN1 S2 (D Et + 10u Mw),  |beta' - beta| <= SN1 S1 (D Et + 10u Mw)
+// The filter uses a = 7u SN1 (V + O), b = 6u SN1 D, Et = 2.5 (a + b|t'|)|rcp| + 4u|t'| and
+// Ea = Ka (1.25 D Et + 14u Mw) with Ka = SN1 S2, Kb = SN1 S1 rounded up on the host (slack >= 15%
+// over every bound: it also covers the rounding of these bound computations and the f64 test's own
+// rounding errors, which are ~2^-29 of the f32 ones), plus absolute floors (2^-80 in a and b, 2^-50
+// in Ea, Eb) for underflow. A rejection needs a TRUE strict comparison against a bound rounded in
+// f32 (x > RN(1 + Ea) implies x > 1 + Ea), so NaN / inf anywhere (0/0, overflowed bounds) keeps
+// the quad a candidate. Valid for |v_k|, |s1_k|, |s2_k|, |o_k| <= 2^30, SN1 in [2^-64, 2^40] per
+// quad (the host sets the scene flag), and D in [2^-30, 2^30] per ray (quad_ray32_ok).
+#pragma once
+
+#include <cmath>
+#include <cstdint>
+
+#ifndef CRT_HD
+#define CRT_HD inline
+#endif
+
+namespace crt {
+
+// one f32 parallelogram record (64 bytes, four 16-byte loads)
+struct alignas(16) DevQuadF {
+    float v[3], s1[3], s2[3], sn[3];
+    float sn1;      // |sn|_1, rounded up
+    float ka, kb;   // |sn|_1 |s2|_1, |sn|_1 |s1|_1, rounded up
+    float pad;
+};
+static_assert(sizeof(DevQuadF) == 64, "f32 quad record");
+constexpr double kF32QuadMax = 0x1p30;
+
+// the ray in f32 for the filter (per entered leaf)
+struct QuadRay32 {
+    float o[3], d[3];
+    float O, D;      // max |o'_k|, max |d'_k|
+    float b6;        // 6u D (b = SN1 * b6)
+    float tlo, thi;  // f32 bounds with tlo <= t_min, thi >= t_max
+};
+
+constexpr float kU = 0x1p-24f;
+
+// RN32 of x rounded down / up to a float bound (x finite or inf)
+CRT_HD float f32_down(double x) {
+    float f = static_cast<float>(x);
+    if (static_cast<double>(f) > x) f = std::nextafter(f, -INFINITY);
+    return f;
+}
+CRT_HD float f32_up(double x) {
+    float f = static_cast<float>(x);
+    if (static_cast<double>(f) < x) f = std::nextafter(f, INFINITY);
+    return f;
+}
+
+CRT_HD bool quad_ray32_ok(const double o[3], const double d[3]) {
+    bool ok = true;
+    double dm = 0;
+    for (int k = 0; k < 3; ++k) {
+        ok = ok && std::fabs(o[k]) <= kF32QuadMax && std::fabs(d[k]) <= 0x1p30;
+        dm = std::fmax(dm, std::fabs(d[k]));
+    }
+    return ok && dm >= 0x1p-30;
+}
+
+CRT_HD void quad_ray32(const double o[3], const double d[3], double tmin, double tmax, QuadRay32& L) {
+    float O = 0, D = 0;
+    for (int k = 0; k < 3; ++k) {
+        L.o[k] = static_cast<float>(o[k]);
+        L.d[k] = static_cast<float>(d[k]);
+        O = std::fmax(O, std::fabs(L.o[k]));
+        D = std::fmax(D, std::fabs(L.d[k]));
+    }
+    L.O = O;
+    L.D = D;
+    L.b6 = D * (6 * kU);
+    L.tlo = f32_down(tmin);
+    L.thi = f32_up(tmax);
+}
+
+// false only where Parallelogram::hit_by provably misses for t_max (and any smaller t_max);
+// rcp(x) is the hardware reciprocal (within 1 ulp of 1/x)
+template <typename Rcp>
+CRT_HD bool quad_candidate(const DevQuadF& q, const QuadRay32& L, Rcp rcp) {
+    const float vx = q.v[0] - L.o[0], vy = q.v[1] - L.o[1], vz = q.v[2] - L.o[2];
+    const float num = std::fma(q.sn[2], vz, std::fma(q.sn[1], vy, q.sn[0] * vx));
+    const float den = std::fma(q.sn[2], L.d[2], std::fma(q.sn[1], L.d[1], q.sn[0] * L.d[0]));
+    const float V = std::fmax(std::fmax(std::fabs(q.v[0]), std::fabs(q.v[1])), std::fabs(q.v[2]));
+    const float a = std::fma(q.sn1 * (7 * kU), V + L.O, 0x1p-80f);
+    const float b = std::fma(q.sn1, L.b6, 0x1p-80f);
+    const float r = rcp(den);
+    const float t = num * r;
+    const float at = std::fabs(t);
+    const float Et = std::fma(std::fma(b, at, a), std::fabs(r) * 2.5f, at * (4 * kU));
+    const bool den_ok = std::fabs(den) > 2 * b;
+    const bool t_out = (t + Et < L.tlo) | (t - Et > L.thi);
+    const float wx = std::fma(L.d[0], t, -vx), wy = std::fma(L.d[1], t, -vy), wz = std::fma(L.d[2], t, -vz);
+    // alpha = sn . (w x s2), beta = sn . (s1 x w)
+    const float c1x = std::fma(wy, q.s2[2], -(wz * q.s2[1]));
+    const float c1y = std::fma(wz, q.s2[0], -(wx * q.s2[2]));
+    const float c1z = std::fma(wx, q.s2[1], -(wy * q.s2[0]));
+    const float alpha = std::fma(q.sn[2], c1z, std::fma(q.sn[1], c1y, q.sn[0] * c1x));
+    const float c2x = std::fma(q.s1[1], wz, -(q.s1[2] * wy));
+    const float c2y = std::fma(q.s1[2], wx, -(q.s1[0] * wz));
+    const float c2z = std::fma(q.s1[0], wy, -(q.s1[1] * wx));
+    const float beta = std::fma(q.sn[2], c2z, std::fma(q.sn[1], c2y, q.sn[0] * c2x));
+    const float Mw = std::fma(L.D, at, L.O + V);
+    const float base = std::fma(L.D, Et * 1.25f, Mw * (14 * kU));
+    const float Ea = std::fma(q.ka, base, 0x1p-50f), Eb = std::fma(q.kb, base, 0x1p-50f);
+    const bool a_out = (alpha < -Ea) | (alpha > 1 + Ea);
+    const bool b_out = (beta < -Eb) | (beta > 1 + Eb);
+    return !(den_ok & (t_out | a_out | b_out));
+}
+
+}  // namespace crt

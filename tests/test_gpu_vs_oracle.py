@@ -126,16 +126,19 @@ def test_minmax_slab_equals_reference_selects(crt, monkeypatch, name, seed, kw):
 @pytest.mark.parametrize("name,seed,kw", [
     ("rtow_final", 42, dict(image_w=120, image_h=80, samples_per_pixel=16)),
     ("cornell", None, dict(image_w=64, image_h=64, samples_per_pixel=8, max_depth=100)),
+    ("parallelograms", None, dict(image_w=64, image_h=64, samples_per_pixel=8)),
     ("christmas_tree", None, dict(image_w=96, image_h=54, samples_per_pixel=4)),
 ])
 def test_f32_decisions_equal_f64(crt, monkeypatch, name, seed, kw):
-    """The f32 node test and the packed-f32 sphere filter only prove outcomes of the f64 tests
-    (walk(), sphere_pair_candidates()): frames with every node test and every sphere decided in
-    f64 (CRT_F64_NODES, CRT_F64_SPHERES, read at upload) are bit-identical."""
+    """The f32 node test and the packed-f32 sphere and parallelogram filters only prove outcomes
+    of the f64 tests (walk(), sphere_pair_candidates(), quad_candidate()): frames with every node
+    test and every primitive decided in f64 (CRT_F64_NODES, CRT_F64_SPHERES, CRT_F64_QUADS, read at
+    upload) are bit-identical."""
     d = scene(crt, name, seed, **kw)
     fast = gpu(crt, d, 41)
     monkeypatch.setenv("CRT_F64_NODES", "1")
     monkeypatch.setenv("CRT_F64_SPHERES", "1")
+    monkeypatch.setenv("CRT_F64_QUADS", "1")
     slow = gpu(crt, d, 41)
     assert np.array_equal(fast, slow)
 
