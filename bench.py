@@ -212,7 +212,7 @@ def main():
         workload += " (BASELINE config 2)"
     # HBM bytes per launch from the rocprofv3 PMC passes (FETCH_SIZE x2 + WRITE_SIZE, the guide's
     # gfx950 correction; tools/gpu_pmc.sh + tools/pmc_summary.py) of this workload on this kernel
-    traffic, traffic_src = None, None
+    traffic, traffic_src, valu = None, None, None
     pmc = Path(args.pmc_json)
     if pmc.exists() and world == 1:
         try:
@@ -220,6 +220,11 @@ def main():
             if pj.get("workload") == workload and pj.get("kernel_source_sha") == kernel_source_sha():
                 traffic = pj.get("hbm_bytes_per_launch")
                 traffic_src = str(pmc.relative_to(ROOT)) if pmc.is_relative_to(ROOT) else str(pmc)
+                if "valu_issue_frac" in pj:
+                    # what actually binds: VALU issue (2 SIMD32 cycles per wave64 instruction, 4 for
+                    # f64) over the chip's SIMD-cycles, and the share of lanes active per instruction
+                    valu = {"issue_frac": round(pj["valu_issue_frac"], 4),
+                            "lane_util": round(pj.get("valu_lane_utilization", 0.0), 4)}
         except Exception:
             traffic = None
 
@@ -247,7 +252,7 @@ def main():
                        "RCCL all-gather of tiles overlapped with the next frame" if distributed else "whole frame on one GPU"},
             "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved_gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "traffic_source": traffic_src,
+                         "traffic_source": traffic_src, "valu": valu,
                          "kernel_ms": round(kernel_ms, 3),
                          "alg_bytes_per_launch": int(alg_bytes),
                          "basis": "SURVEY 8d algorithmic bytes (56 B/node, 36 B/sphere test, 124 B/quad test, "
