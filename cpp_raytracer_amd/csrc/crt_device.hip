@@ -116,6 +116,9 @@ struct Counters {
     unsigned long long it_walk, it_leaf, it_shade;  // wave iterations (lane utilization)
     unsigned long long slow_nodes, it_slow;  // node tests decided in f64 (lanes / wave iterations)
     unsigned long long cand, it_cand;        // two-pass leaves: exact tests of candidates (lanes / wave iterations)
+    // per traversal round (walk + leaf): rounds, lanes walking at its start, lanes holding a leaf
+    // after the walk, lanes with a finished ray after the leaf step (CRT_DEBUG_COUNTERS)
+    unsigned long long rounds, round_walkers, round_leaves, round_done, shade_rounds;
 };
 
 // one lane's counts in the instrumented pass, added to the Counters when the lane ends; 64-bit:
@@ -1404,6 +1407,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LSCENE ?
         // traversal rounds (walk to the next entered leaf, test it) until enough lanes hold a
         // finished ray, or none is traversing
         while (true) {
+            if (COUNT) {
+                const unsigned long long nw = __popcll(__ballot(R.state == kWalk));
+                if (wave_leader()) {
+                    atomicAdd(&counters->rounds, 1ull);
+                    atomicAdd(&counters->round_walkers, nw);
+                }
+            }
             if (COUNT) cw -= static_cast<uint32_t>(wall_clock64());
             if (!W.exact_slab && __ballot(R.state == kWalk && (R.neg & kZeroDir)) == 0) {
                 if (R.state == kWalk) walk<SE, COUNT, false, kTopTreelet && !LSCENE, LSCENE, GSTACK>(S, st, P.o, P.d, C.t_min, tmin32, R, ctr);
@@ -1411,18 +1421,24 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LSCENE ?
                 if (R.state == kWalk) walk<SE, COUNT, true, kTopTreelet && !LSCENE, LSCENE, GSTACK>(S, st, P.o, P.d, C.t_min, tmin32, R, ctr);
             }
             if (COUNT) cw += static_cast<uint32_t>(wall_clock64());
+            if (COUNT) {
+                const unsigned long long nl = __popcll(__ballot(R.state == kLeaf));
+                if (wave_leader()) atomicAdd(&counters->round_leaves, nl);
+            }
             if (COUNT) cl -= static_cast<uint32_t>(wall_clock64());
             if (R.state == kLeaf) leaf_step<SE, COUNT, kTopTreelet && !LSCENE, LSCENE>(S, st, P.o, P.d, C.t_min, W.sphere_only != 0, W.spheres_f32 != 0, W.quads_f32 != 0, R, ctr);
             if (COUNT) cl += static_cast<uint32_t>(wall_clock64());
             const uint64_t pending = __ballot(R.state == kWalk);
             const uint64_t finished = __ballot(R.state == kDone);
             const int nfin = __popcll(finished);
+            if (COUNT && wave_leader()) atomicAdd(&counters->round_done, static_cast<unsigned long long>(nfin));
             if (pending == 0 || nfin >= kShadeBatch || (__popcll(pending) <= kPendingMax && nfin >= kShadeMin)) break;
         }
         const uint64_t m_done = __ballot(R.state == kDone);
         if (COUNT && t_first_idle == 0 && __ballot(R.state == kIdle) != 0) t_first_idle = wall_clock64();
         if (m_done == 0) break;  // every lane idle: the queue is dry
         if (COUNT) cs -= static_cast<uint32_t>(wall_clock64());
+        if (COUNT && wave_leader()) atomicAdd(&counters->shade_rounds, 1ull);
         if (R.state == kDone) {
             if (COUNT && wave_leader()) ctr.it_shade++;
             bool ended = shade<LSCENE>(S, CL, P, R.found, R.ref, R.tmax, acc);
@@ -1962,8 +1978,11 @@ static int launch_render(const crt_scene* s, int device, const crt_camera* cam, 
         count_stats->wave_iters_candidates = h.it_cand;
         if (std::getenv("CRT_DEBUG_COUNTERS"))
             std::fprintf(stderr, "crt counters: rays %llu nodes %llu sphere_tests %llu quad_tests %llu it_walk %llu "
-                         "it_leaf %llu it_shade %llu\n", h.rays, h.nodes, h.sphere_tests, h.quad_tests, h.it_walk,
-                         h.it_leaf, h.it_shade);
+                         "it_leaf %llu it_shade %llu rounds %llu walkers/round %.2f leaves/round %.2f done/round %.2f "
+                         "shade_rounds %llu\n", h.rays, h.nodes, h.sphere_tests, h.quad_tests, h.it_walk,
+                         h.it_leaf, h.it_shade, h.rounds, double(h.round_walkers) / double(h.rounds ? h.rounds : 1),
+                         double(h.round_leaves) / double(h.rounds ? h.rounds : 1),
+                         double(h.round_done) / double(h.rounds ? h.rounds : 1), h.shade_rounds);
     }
     return CRT_OK;
 }
