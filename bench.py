@@ -46,7 +46,7 @@ def kernel_source_sha() -> str:
     roofline.traffic only when it was collected on this exact kernel."""
     import hashlib
     h = hashlib.sha256()
-    for f in ("crt_device.hip", "crt_internal.h"):
+    for f in ("crt_device.hip", "crt_internal.h", "crt_quad_filter.h"):
         h.update((ROOT / "cpp_raytracer_amd" / "csrc" / f).read_bytes())
     return h.hexdigest()[:16]
 

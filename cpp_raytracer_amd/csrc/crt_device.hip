@@ -121,15 +121,34 @@ struct Counters {
     unsigned long long rounds, round_walkers, round_leaves, round_done, shade_rounds;
 };
 
-// one lane's counts in the instrumented pass, added to the Counters when the lane ends; 64-bit:
-// a lane of the persistent grid traces units for the whole launch (a one-block grid on a large
-// frame would wrap 32-bit counts)
+// one lane's counts in the instrumented pass, added to the 64-bit Counters when the lane ends, and
+// before then whenever one of them passes 2^31 (flush_counts, once per shade round): a lane of the
+// persistent grid traces units for the whole launch, and a small grid on a large frame would wrap
+// 32-bit counts (64-bit lane counts would cost the instrumented kernel spills)
 struct LaneCounters {
-    unsigned long long rays, nodes, sphere_tests, quad_tests;
-    unsigned long long it_walk, it_leaf, it_shade;
-    unsigned long long slow_nodes, it_slow;
-    unsigned long long cand, it_cand;
+    uint32_t rays, nodes, sphere_tests, quad_tests;
+    uint32_t it_walk, it_leaf, it_shade;
+    uint32_t slow_nodes, it_slow;
+    uint32_t cand, it_cand;
 };
+
+// adds a lane's counts to the launch's totals and clears them (iteration counters are incremented
+// by whichever lane led that iteration)
+__device__ __forceinline__ void flush_counts(LaneCounters& c, Counters* t) {
+    using ull = unsigned long long;
+    atomicAdd(&t->rays, static_cast<ull>(c.rays));
+    atomicAdd(&t->nodes, static_cast<ull>(c.nodes));
+    atomicAdd(&t->sphere_tests, static_cast<ull>(c.sphere_tests));
+    atomicAdd(&t->quad_tests, static_cast<ull>(c.quad_tests));
+    atomicAdd(&t->it_walk, static_cast<ull>(c.it_walk));
+    atomicAdd(&t->it_leaf, static_cast<ull>(c.it_leaf));
+    atomicAdd(&t->it_shade, static_cast<ull>(c.it_shade));
+    atomicAdd(&t->slow_nodes, static_cast<ull>(c.slow_nodes));
+    atomicAdd(&t->it_slow, static_cast<ull>(c.it_slow));
+    atomicAdd(&t->cand, static_cast<ull>(c.cand));
+    atomicAdd(&t->it_cand, static_cast<ull>(c.it_cand));
+    c = LaneCounters{};
+}
 
 // counts one per wave: only the lowest active lane increments
 __device__ __forceinline__ bool wave_leader() {
@@ -985,9 +1004,11 @@ __device__ __forceinline__ void leaf_step(const SceneView& S, Stack<SE>& st, con
                 R.found = true;
             }
         }
-    } else if (qfilter && range.y <= 32 && quad_ray32_ok(o, d)) {
+    } else if (LS && qfilter && range.y <= 32 && quad_ray32_ok(o, d)) {
         // parallelogram-only scenes (a slot is its parallelogram's index): the same two passes,
-        // with the f32 filter of crt_quad_filter.h (quad_candidate) in pass 1
+        // with the f32 filter of crt_quad_filter.h (quad_candidate) in pass 1. LDS-scene kernels
+        // only: in the HBM-scene kernels its registers cost spills (none of the reference's
+        // parallelogram-only scenes is that large)
         QuadRay32 L;
         quad_ray32(o, d, tmin, R.tmax, L);
         uint32_t cand = 0;
@@ -1259,6 +1280,12 @@ constexpr int kShadeMin = CRT_SHADE_MIN, kPendingMax = CRT_PENDING_MAX;
 #define CRT_TOP_TREELET 1
 #endif
 constexpr bool kTopTreelet = CRT_TOP_TREELET != 0;
+// per-round lane counts in the instrumented pass (printed under CRT_DEBUG_COUNTERS); off by default:
+// their atomics shift the instrumented pass's phase timings
+#ifndef CRT_ROUND_COUNTERS
+#define CRT_ROUND_COUNTERS 0
+#endif
+constexpr bool kRoundCounters = CRT_ROUND_COUNTERS != 0;
 
 template <typename SE, bool GSTACK, bool LSCENE, bool COUNT>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LSCENE ? CRT_WAVES_PER_EU_LDS : CRT_WAVES_PER_EU, 8))) void render_kernel(
@@ -1407,7 +1434,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LSCENE ?
         // traversal rounds (walk to the next entered leaf, test it) until enough lanes hold a
         // finished ray, or none is traversing
         while (true) {
-            if (COUNT) {
+            if (COUNT && kRoundCounters) {
                 const unsigned long long nw = __popcll(__ballot(R.state == kWalk));
                 if (wave_leader()) {
                     atomicAdd(&counters->rounds, 1ull);
@@ -1421,7 +1448,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LSCENE ?
                 if (R.state == kWalk) walk<SE, COUNT, true, kTopTreelet && !LSCENE, LSCENE, GSTACK>(S, st, P.o, P.d, C.t_min, tmin32, R, ctr);
             }
             if (COUNT) cw += static_cast<uint32_t>(wall_clock64());
-            if (COUNT) {
+            if (COUNT && kRoundCounters) {
                 const unsigned long long nl = __popcll(__ballot(R.state == kLeaf));
                 if (wave_leader()) atomicAdd(&counters->round_leaves, nl);
             }
@@ -1431,14 +1458,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LSCENE ?
             const uint64_t pending = __ballot(R.state == kWalk);
             const uint64_t finished = __ballot(R.state == kDone);
             const int nfin = __popcll(finished);
-            if (COUNT && wave_leader()) atomicAdd(&counters->round_done, static_cast<unsigned long long>(nfin));
+            if (COUNT && kRoundCounters && wave_leader()) atomicAdd(&counters->round_done, static_cast<unsigned long long>(nfin));
             if (pending == 0 || nfin >= kShadeBatch || (__popcll(pending) <= kPendingMax && nfin >= kShadeMin)) break;
         }
         const uint64_t m_done = __ballot(R.state == kDone);
         if (COUNT && t_first_idle == 0 && __ballot(R.state == kIdle) != 0) t_first_idle = wall_clock64();
         if (m_done == 0) break;  // every lane idle: the queue is dry
         if (COUNT) cs -= static_cast<uint32_t>(wall_clock64());
-        if (COUNT && wave_leader()) atomicAdd(&counters->shade_rounds, 1ull);
+        if (COUNT && kRoundCounters && wave_leader()) atomicAdd(&counters->shade_rounds, 1ull);
+        if (COUNT && ((ctr.rays | ctr.nodes | ctr.sphere_tests | ctr.quad_tests | ctr.it_walk | ctr.it_leaf |
+                       ctr.it_shade | ctr.slow_nodes | ctr.it_slow | ctr.cand | ctr.it_cand) & 0x80000000u))
+            flush_counts(ctr, counters);
         if (R.state == kDone) {
             if (COUNT && wave_leader()) ctr.it_shade++;
             bool ended = shade<LSCENE>(S, CL, P, R.found, R.ref, R.tmax, acc);
@@ -1472,10 +1502,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LSCENE ?
     }
     if (COUNT) {
         using ull = unsigned long long;
-        atomicAdd(&counters->rays, static_cast<ull>(ctr.rays));
-        atomicAdd(&counters->nodes, static_cast<ull>(ctr.nodes));
-        atomicAdd(&counters->sphere_tests, static_cast<ull>(ctr.sphere_tests));
-        atomicAdd(&counters->quad_tests, static_cast<ull>(ctr.quad_tests));
+        flush_counts(ctr, counters);
         if (lane == 0) {  // per-wave phase times (the wave executes each phase as one)
             atomicAdd(&counters->cyc_walk, static_cast<ull>(cw));
             atomicAdd(&counters->cyc_leaf, static_cast<ull>(cl));
@@ -1484,14 +1511,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LSCENE ?
             atomicAdd(&counters->cyc_total, t_end - t_start);
             atomicAdd(&counters->cyc_tail, t_first_idle ? t_end - t_first_idle : 0ull);
         }
-        // iteration counters are incremented by whichever lane led that iteration
-        atomicAdd(&counters->it_walk, static_cast<ull>(ctr.it_walk));
-        atomicAdd(&counters->it_leaf, static_cast<ull>(ctr.it_leaf));
-        atomicAdd(&counters->it_shade, static_cast<ull>(ctr.it_shade));
-        atomicAdd(&counters->slow_nodes, static_cast<ull>(ctr.slow_nodes));
-        atomicAdd(&counters->it_slow, static_cast<ull>(ctr.it_slow));
-        atomicAdd(&counters->cand, static_cast<ull>(ctr.cand));
-        atomicAdd(&counters->it_cand, static_cast<ull>(ctr.it_cand));
     }
 }
 
