@@ -91,7 +91,13 @@ struct Work {
     // work queue, taken in order by the waves of a persistent grid (render_kernel): bulk items
     // (tile i / groups, chunks [(i % groups) * item_chunks, + item_chunks)), then tail items
     // (tile j / tail_chunks, chunk bulk_chunks + j % tail_chunks); 64 units per chunk
-    uint32_t* queue;        // the next item (zeroed before the launch)
+    // XCD-local queues (v12): the band's tiles (tile-major) are cut into `segments` contiguous
+    // ranges, segment x = tiles [tiles * x / segments, tiles * (x + 1) / segments), each with its own
+    // counter queue[x] (zeroed before the launch) over its items: its tiles' bulk items, then its
+    // tiles' tail items. A wave starts on segment blockIdx % segments (blocks b and b + 8 share an
+    // XCD and its L2) and moves on to the next segments when its own is dry.
+    uint32_t* queue;
+    uint32_t segments;      // 8, or 1 (CRT_XCD_QUEUES=0)
     uint32_t n_items, bulk_items;
     uint32_t item_chunks, groups, bulk_chunks, tail_chunks;
     uint32_t rb_shift;      // log2(row_block) when it is a power of two, else 32
@@ -1347,7 +1353,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LSCENE ?
     // The wave's current item (wave-uniform) and how many of its 64 units are drawn; lanes take
     // the next units in lane order. A unit's sum goes to partial[chunk][pixel] whichever lane
     // traced it, so frames do not depend on the schedule.
-    uint32_t item = 0, item_pos = 0, item_units = 0;
+    uint32_t item_pos = 0, item_units = 0;
+    uint32_t seg = blockIdx.x % W.segments, seg_tried = 0;  // the wave's queue (XCD-local first)
     uint32_t item_txy = 0, item_chunk = 0;
     // the lane's unit: tile (tx | ty << 16), chunk << 6 | tile pixel; and its current sample
     uint32_t u_txy = 0, u_cp = 0, s = 0;
@@ -1365,28 +1372,39 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LSCENE ?
         while (true) {
             const uint64_t m = __ballot(need);
             if (m == 0) break;
-            if (item_pos >= item_units) {  // the item is used up: the next one from the queue
+            if (item_pos >= item_units) {  // the item is used up: the next one from a queue
                 const uint32_t leader = static_cast<uint32_t>(__ffsll(static_cast<long long>(m)) - 1);
-                uint32_t v = 0;
-                if (lane == leader) v = atomicAdd(W.queue, 1u);
-                item = __builtin_amdgcn_readlane(v, leader);
+                item_units = 0;
                 item_pos = 0;
-                if (item < W.n_items) {
-                    uint32_t tile;
-                    if (item < W.bulk_items) {
-                        tile = item / W.groups;
-                        item_chunk = (item - tile * W.groups) * W.item_chunks;
-                        item_units = 64 * W.item_chunks;
-                    } else {
-                        const uint32_t j = item - W.bulk_items;
-                        tile = j / W.tail_chunks;
-                        item_chunk = W.bulk_chunks + (j - tile * W.tail_chunks);
-                        item_units = 64;
+                // this wave's segment first, then the others in turn; seg == segments: all dry
+                while (seg < W.segments) {
+                    const uint32_t t0 = static_cast<uint32_t>(static_cast<uint64_t>(W.tiles) * seg / W.segments);
+                    const uint32_t t1 = static_cast<uint32_t>(static_cast<uint64_t>(W.tiles) * (seg + 1) / W.segments);
+                    const uint32_t nt = t1 - t0, bulk = nt * W.groups;
+                    uint32_t v = 0;
+                    if (lane == leader) v = atomicAdd(W.queue + seg, 1u);
+                    const uint32_t j = __builtin_amdgcn_readlane(v, leader);
+                    if (j < nt * (W.groups + W.tail_chunks)) {
+                        uint32_t tile;
+                        if (j < bulk) {
+                            tile = j / W.groups;
+                            item_chunk = (j - tile * W.groups) * W.item_chunks;
+                            item_units = 64 * W.item_chunks;
+                        } else {
+                            const uint32_t jt = j - bulk;
+                            tile = jt / W.tail_chunks;
+                            item_chunk = W.bulk_chunks + (jt - tile * W.tail_chunks);
+                            item_units = 64;
+                        }
+                        tile += t0;
+                        item_txy = (tile % W.tiles_x) | ((tile / W.tiles_x) << 16);
+                        break;
                     }
-                    item_txy = (tile % W.tiles_x) | ((tile / W.tiles_x) << 16);
+                    if (++seg_tried >= W.segments) seg = W.segments;  // every segment is dry
+                    else seg = seg + 1 == W.segments ? 0 : seg + 1;
                 }
             }
-            if (item >= W.n_items) {  // the queue is dry
+            if (item_units == 0) {  // the queues are dry
                 need = false;
                 break;
             }
@@ -1947,7 +1965,11 @@ static int launch_render(const crt_scene* s, int device, const crt_camera* cam, 
             if (items >= 0xffffffffull) return fail(CRT_E_INVALID, "band too large for one launch");
             W.n_items = static_cast<uint32_t>(items);
             W.bulk_items = static_cast<uint32_t>(bulk_items);
-            HIP_TRY(hipMemsetAsync(queue, 0, sizeof(uint32_t), stream));
+            // HBM-resident scenes: one queue per XCD (blocks b and b + 8 share one), so an XCD's L2
+            // serves the rays of one region of the band (config 4: 163.5 vs 166.2 ms); LDS scenes
+            // keep one queue (config 2: 88.5 vs 89.0 ms with eight). CRT_XCD_QUEUES=0/1 forces.
+            W.segments = knob("CRT_XCD_QUEUES", LSCENE ? 0 : 1) ? 8u : 1u;
+            HIP_TRY(hipMemsetAsync(queue, 0, 8 * sizeof(uint32_t), stream));
             if (count) {
                 hipLaunchKernelGGL((dev::render_kernel<SE, GSTACK, LSCENE, true>), dim3(static_cast<uint32_t>(blocks)),
                                    dim3(dev::kBlock), lds, stream, S, C, W, partial, gstack, ctr);
