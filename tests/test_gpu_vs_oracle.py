@@ -154,6 +154,20 @@ def test_work_queue_schedule_does_not_change_frames(crt, monkeypatch, spp):
     for blocks in (1, 3, 37):
         monkeypatch.setenv("CRT_GRID_BLOCKS", str(blocks))
         assert np.array_equal(base, gpu(crt, d, 43)), blocks
+    # eight XCD-local segment queues with stealing (the HBM-scene default) vs one queue
+    for blocks in (3, 1000):
+        monkeypatch.setenv("CRT_GRID_BLOCKS", str(blocks))
+        monkeypatch.setenv("CRT_XCD_QUEUES", "1")
+        assert np.array_equal(base, gpu(crt, d, 43)), ("xcd", blocks)
+
+
+def test_xcd_queues_do_not_change_hbm_frames(crt, monkeypatch):
+    """The HBM-scene kernels take work from eight segment queues (one per XCD); one queue gives the
+    same frame bit for bit."""
+    d = scene(crt, "christmas_tree", image_w=96, image_h=54, samples_per_pixel=8)
+    base = gpu(crt, d, 46)
+    monkeypatch.setenv("CRT_XCD_QUEUES", "0")
+    assert np.array_equal(base, gpu(crt, d, 46))
 
 
 @pytest.mark.parametrize("name,seed", [("rtow_final", 42), ("cornell", None), ("christmas_tree", None),
