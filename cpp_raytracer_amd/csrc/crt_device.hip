@@ -125,6 +125,7 @@ struct Counters {
     // per traversal round (walk + leaf): rounds, lanes walking at its start, lanes holding a leaf
     // after the walk, lanes with a finished ray after the leaf step (CRT_DEBUG_COUNTERS)
     unsigned long long rounds, round_walkers, round_leaves, round_done, shade_rounds;
+    unsigned long long cyc_draw, cyc_init;  // wave ticks drawing units / starting paths + traversal set-up
 };
 
 // one lane's counts in the instrumented pass, added to the 64-bit Counters when the lane ends, and
@@ -704,20 +705,10 @@ __device__ __forceinline__ bool finite_nonzero(double x) { return fabs(x) < __bu
 __device__ __forceinline__ bool finite(double x) { return fabs(x) < __builtin_inf(); }
 __device__ __forceinline__ float tmax_f32(double t) { return static_cast<float>(fmin(t, 0x1p100)); }
 
-// 1/x within 2^-51 relative for 2^-1000 <= |x| <= 2^1000: v_rcp_f64 and two Newton steps (the
-// first steps of hipcc's own f64 division, without its scaling and final correction). The walk's
-// f32 node test only needs RN32(1/d) and RN32(o/d) within its error analysis, which has room for
-// it (walk()); the f64 decisions (slab64, the EXACT walk) divide exactly.
-__device__ __forceinline__ double recip_nr(double x) {
-    double r = __builtin_amdgcn_rcp(x);
-    r = fma(r, fma(-x, r, 1.0), r);
-    return fma(r, fma(-x, r, 1.0), r);
-}
 __device__ __forceinline__ bool dir_ok(double x) { return fabs(x) >= 0x1p-1000 && fabs(x) <= 0x1p1000; }
 
 // f32_ok: the scene's node bounds fit the f32 error analysis (Work::f32_ok)
 __device__ __forceinline__ void trav_init(const double o[3], const double d[3], bool f32_ok, Trav& R) {
-    const double inv[3] = {recip_nr(d[0]), recip_nr(d[1]), recip_nr(d[2])};
     R.a = d[0] * d[0] + d[1] * d[1] + d[2] * d[2];
     R.tmax = __builtin_inf();
     R.tmax32 = 0x1p100f;
@@ -730,20 +721,23 @@ __device__ __forceinline__ void trav_init(const double o[3], const double d[3], 
     const bool fast = dir_ok(d[0]) && dir_ok(d[1]) && dir_ok(d[2]) &&
                       finite(o[0]) && finite(o[1]) && finite(o[2]);
     R.neg = (d[0] < 0 ? 1u : 0u) | (d[1] < 0 ? 2u : 0u) | (d[2] < 0 ? 4u : 0u) | (fast ? 0u : kZeroDir);
-    // the f32 node test's error analysis (walk()) holds for 2^-40 <= |1/d_k| <= 2^40 and
-    // |o_k| <= 2^40, here ensured by 2^-39 <= |d_k| <= 2^39; other rays get marg = inf, i.e.
-    // every node test decided in f64
+    // The f32 walk's ray constants, in f32 (v12): inv32 = v_rcp_f32(RN32(d)) (within 1 ulp of
+    // 1/RN32(d), so within 3.01u of 1/d), oinv32 = RN32(RN32(o) * inv32) (within 5.02u of o/d);
+    // walk() bounds the resulting slab values for these. The analysis holds for
+    // 2^-40 <= |1/d_k| <= 2^40 and |o_k| <= 2^40, here ensured by 2^-39 <= |RN32(d_k)| <= 2^39;
+    // other rays get marg = inf, i.e. every node test decided in f64.
     bool f32 = f32_ok;
-    double A = 0;
+    float A = 0;
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-        const double oi = o[k] * inv[k];
-        R.inv32[k] = static_cast<float>(inv[k]);
-        R.oinv32[k] = static_cast<float>(oi);
-        A = fmax(A, fabs(oi));
-        f32 = f32 && fabs(d[k]) <= 0x1p39 && fabs(d[k]) >= 0x1p-39 && fabs(o[k]) <= 0x1p40;
+        const float d32 = static_cast<float>(d[k]), o32 = static_cast<float>(o[k]);
+        R.inv32[k] = __builtin_amdgcn_rcpf(d32);
+        R.oinv32[k] = o32 * R.inv32[k];
+        A = __builtin_fmaxf(A, __builtin_fabsf(R.oinv32[k]));
+        f32 = f32 && __builtin_fabsf(d32) <= 0x1p39f && __builtin_fabsf(d32) >= 0x1p-39f &&
+              __builtin_fabsf(o32) <= 0x1p40f;
     }
-    R.marg = f32 ? static_cast<float>(fmax(A * 0x1p-19, 0x1p-60)) : __builtin_inff();
+    R.marg = f32 ? __builtin_fmaxf(A * 0x1p-19f, 0x1p-60f) : __builtin_inff();
     R.state = kWalk;
     R.found = false;
 }
@@ -765,16 +759,17 @@ __device__ __forceinline__ void trav_init(const double o[3], const double d[3], 
 // take the EXACT variant: the reference's select sequence verbatim on the f64 node.
 //
 // The other rays decide the test in f32 first (Trav::inv32 / oinv32 / marg, DevNodeF):
-//   t'_jk = fma(b32_jk, inv32_k, -oinv32_k),  b32 = RN32(b), inv32 = RN32(inv~), oinv32 =
-//   RN32(RN(o * inv~)), inv~ = recip_nr(d) within 2^-51 of the f64 inv (its extra error, below
-//   2^-27 u (|b| + |o|) |inv|, is inside the 0.01 u of slack below). With u = 2^-24 and A = max_k |o_k inv_k|, and |b| <= |b - o| + |o|,
-//   |t' - t| <= 3.01 u (|b| + |o|) |inv| + 2.01 u64 |t| <= 2^-22.4 |t'| + 2^-21.4 A + 2^-85
+//   t'_jk = fma(b32_jk, inv32_k, -oinv32_k),  b32 = RN32(b), inv32 = v_rcp_f32(RN32(d)) within
+//   3.01u of inv = 1/d, oinv32 = RN32(RN32(o) * inv32) within 5.02u of o inv (trav_init; u =
+//   2^-24). With A = max_k |o_k inv_k| and |b| <= |b - o| + |o|:
+//   |t' - t| <= 4.01u |b||inv| + 5.02u |o||inv| + u |t'| + 2.01 u64 |t|
+//            <= 5.02u |t'| + 9.04u A + 2^-85 = 2^-21.7 |t'| + 2^-20.8 A + 2^-85
 // (2^-85: f32 underflow at |inv| <= 2^40). min / max are 1-Lipschitz, so lo' = max(near', tmin')
 // and hi' = min(far', tmax') are within that bound of lo = max(near, tmin), hi = min(far, tmax)
-// with |t'| <= M = max(|lo'|, |hi'|) (tmin', tmax' are RN32 of tmin, tmax; tmax' = 2^100 for
-// larger tmax never binds, as |t'| < 2^82 here), and gap' = RN32(hi' - lo') is within
-// 2^-21 M + 2^-20.4 A + 2^-84 of gap = hi - lo. So with th = 2^-19 M + marg, marg =
-// max(2^-19 A, 2^-60):
+// with |t'| <= M = max(|lo'|, |hi'|) (tmin', tmax' are RN32 of tmin, tmax, within u M; tmax' =
+// 2^100 for larger tmax never binds, as |t'| < 2^82 here), and gap' = RN32(hi' - lo') is within
+// 14.1u M + 18.1u A + 2^-84 <= 2^-20.1 M + 2^-19.8 A + 2^-84 of gap = hi - lo. So with
+// th = 2^-19 M + marg, marg = max(2^-19 A', 2^-60), A' = max_k |oinv32_k| >= A (1 - 5.1u):
 //   gap' >  th  =>  gap > 0: far > near, near < tmax, far > tmin  (enter)
 //   gap' < -th  =>  gap < 0: far < near, far < tmin or tmax < near (no entry)
 // and only lanes with |gap'| <= th (grazing rays, ties, rays with marg = inf) run the f64 test on
@@ -1286,6 +1281,30 @@ constexpr int kShadeMin = CRT_SHADE_MIN, kPendingMax = CRT_PENDING_MAX;
 #define CRT_TOP_TREELET 1
 #endif
 constexpr bool kTopTreelet = CRT_TOP_TREELET != 0;
+// Static wave priority per phase (s_setprio 0-3; the SQ issues a ready instruction of the highest
+// priority wave first, then the oldest): the traversal phases are dependency chains (LDS read ->
+// test -> next address), the shade and path-start phases have more independent work to fill in.
+// Config 2 (ms/frame, one box): none 87.9; walk 1 86.6; walk+leaf 1 85.6; walk 2 / leaf 1 85.6;
+// walk 1 / leaf 2 85.6; walk 2 / leaf 2 / start 1 85.4; walk 3 / leaf 2 / start 1 (kept) 85.3;
+// walk 1 / leaf 1 / start 1 86.0.
+#ifndef CRT_PRIO_WALK
+#define CRT_PRIO_WALK 3
+#endif
+#ifndef CRT_PRIO_LEAF
+#define CRT_PRIO_LEAF 2
+#endif
+#ifndef CRT_PRIO_SHADE
+#define CRT_PRIO_SHADE 0
+#endif
+#ifndef CRT_PRIO_INIT
+#define CRT_PRIO_INIT 1
+#endif
+constexpr int kPrioWalk = CRT_PRIO_WALK, kPrioLeaf = CRT_PRIO_LEAF, kPrioShade = CRT_PRIO_SHADE,
+              kPrioInit = CRT_PRIO_INIT;
+template <int P>
+__device__ __forceinline__ void set_prio() {
+    if constexpr (kPrioWalk || kPrioLeaf || kPrioShade || kPrioInit) __builtin_amdgcn_s_setprio(P);
+}
 // per-round lane counts in the instrumented pass (printed under CRT_DEBUG_COUNTERS); off by default:
 // their atomics shift the instrumented pass's phase timings
 #ifndef CRT_ROUND_COUNTERS
@@ -1364,11 +1383,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LSCENE ?
     R.state = kIdle;
     bool need = true, start = false, cont = false;
     uint32_t cw = 0, cl = 0, cs = 0;  // wall_clock64 ticks (100 MHz), differences mod 2^32
+    uint32_t cd = 0, ci = 0;
     unsigned long long t_first_idle = 0;
     while (true) {
         // lanes without a unit draw until each holds a unit with samples to trace or the queue
         // is dry. A unit off the image has no pixel sum; one with max_depth == 0 sums
         // RGB::zero() (camera.h:211-213) and is written at once.
+        if (COUNT) cd -= static_cast<uint32_t>(wall_clock64());
+        set_prio<kPrioInit>();
         while (true) {
             const uint64_t m = __ballot(need);
             if (m == 0) break;
@@ -1433,6 +1455,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LSCENE ?
             }
             item_pos += take;
         }
+        if (COUNT) {
+            const uint32_t now = static_cast<uint32_t>(wall_clock64());
+            cd += now;
+            ci -= now;
+        }
         if (start) {
             const uint32_t pix = u_cp & 63;
             const uint32_t col = W.col0 + (u_txy & 0xffffu) * kTileW + pix % kTileW;
@@ -1449,6 +1476,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LSCENE ?
         }
         start = false;
         cont = false;
+        if (COUNT) ci += static_cast<uint32_t>(wall_clock64());
         // traversal rounds (walk to the next entered leaf, test it) until enough lanes hold a
         // finished ray, or none is traversing
         while (true) {
@@ -1460,12 +1488,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LSCENE ?
                 }
             }
             if (COUNT) cw -= static_cast<uint32_t>(wall_clock64());
+            set_prio<kPrioWalk>();
             if (!W.exact_slab && __ballot(R.state == kWalk && (R.neg & kZeroDir)) == 0) {
                 if (R.state == kWalk) walk<SE, COUNT, false, kTopTreelet && !LSCENE, LSCENE, GSTACK>(S, st, P.o, P.d, C.t_min, tmin32, R, ctr);
             } else {
                 if (R.state == kWalk) walk<SE, COUNT, true, kTopTreelet && !LSCENE, LSCENE, GSTACK>(S, st, P.o, P.d, C.t_min, tmin32, R, ctr);
             }
             if (COUNT) cw += static_cast<uint32_t>(wall_clock64());
+            set_prio<kPrioLeaf>();
             if (COUNT && kRoundCounters) {
                 const unsigned long long nl = __popcll(__ballot(R.state == kLeaf));
                 if (wave_leader()) atomicAdd(&counters->round_leaves, nl);
@@ -1483,6 +1513,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LSCENE ?
         if (COUNT && t_first_idle == 0 && __ballot(R.state == kIdle) != 0) t_first_idle = wall_clock64();
         if (m_done == 0) break;  // every lane idle: the queue is dry
         if (COUNT) cs -= static_cast<uint32_t>(wall_clock64());
+        set_prio<kPrioShade>();
         if (COUNT && kRoundCounters && wave_leader()) atomicAdd(&counters->shade_rounds, 1ull);
         if (COUNT && ((ctr.rays | ctr.nodes | ctr.sphere_tests | ctr.quad_tests | ctr.it_walk | ctr.it_leaf |
                        ctr.it_shade | ctr.slow_nodes | ctr.it_slow | ctr.cand | ctr.it_cand) & 0x80000000u))
@@ -1525,6 +1556,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LSCENE ?
             atomicAdd(&counters->cyc_walk, static_cast<ull>(cw));
             atomicAdd(&counters->cyc_leaf, static_cast<ull>(cl));
             atomicAdd(&counters->cyc_shade, static_cast<ull>(cs));
+            atomicAdd(&counters->cyc_draw, static_cast<ull>(cd));
+            atomicAdd(&counters->cyc_init, static_cast<ull>(ci));
             const unsigned long long t_end = wall_clock64();
             atomicAdd(&counters->cyc_total, t_end - t_start);
             atomicAdd(&counters->cyc_tail, t_first_idle ? t_end - t_first_idle : 0ull);
@@ -2020,10 +2053,13 @@ static int launch_render(const crt_scene* s, int device, const crt_camera* cam, 
         if (std::getenv("CRT_DEBUG_COUNTERS"))
             std::fprintf(stderr, "crt counters: rays %llu nodes %llu sphere_tests %llu quad_tests %llu it_walk %llu "
                          "it_leaf %llu it_shade %llu rounds %llu walkers/round %.2f leaves/round %.2f done/round %.2f "
-                         "shade_rounds %llu\n", h.rays, h.nodes, h.sphere_tests, h.quad_tests, h.it_walk,
+"shade_rounds %llu; wave time: walk %.3f leaf %.3f shade %.3f draw %.3f init %.3f\n", h.rays, h.nodes, h.sphere_tests, h.quad_tests, h.it_walk,
                          h.it_leaf, h.it_shade, h.rounds, double(h.round_walkers) / double(h.rounds ? h.rounds : 1),
                          double(h.round_leaves) / double(h.rounds ? h.rounds : 1),
-                         double(h.round_done) / double(h.rounds ? h.rounds : 1), h.shade_rounds);
+                         double(h.round_done) / double(h.rounds ? h.rounds : 1), h.shade_rounds,
+                         double(h.cyc_walk) / double(h.cyc_total), double(h.cyc_leaf) / double(h.cyc_total),
+                         double(h.cyc_shade) / double(h.cyc_total), double(h.cyc_draw) / double(h.cyc_total),
+                         double(h.cyc_init) / double(h.cyc_total));
     }
     return CRT_OK;
 }
