@@ -104,6 +104,7 @@ struct Work {
     // LDS layout of the scene-staging kernels (byte offsets / 16-byte padded sizes)
     uint32_t lds_nodes, lds_refs, lds_spheres, lds_quads, lds_quadf, lds_stack;
     uint32_t bytes_nodes, bytes_refs, bytes_spheres, bytes_quads, bytes_quadf;
+    uint32_t lds_sph64, bytes_sph64;  // sphere-only LDS scenes: the f64 spheres too, when they fit
     uint32_t sphere_only;   // every primitive is a sphere: refs[slot] == slot
     uint32_t exact_slab;    // the scene needs walk_step's EXACT variant for every ray
     uint32_t ntop;          // HBM-scene kernels: f32 nodes [0, ntop) bytes staged in LDS at offset 0
@@ -997,7 +998,7 @@ __device__ __forceinline__ void leaf_step(const SceneView& S, Stack<SE>& st, con
             const uint32_t i = range.x + (nbits - 1 - b);
             double t;
             // the f64 spheres are in HBM (L1) in this mode
-            if (hit_sphere<false>(sphere_global(S.spheres + i), o, d, R.a, ia, tmin, R.tmax, lo, hi, t)) {
+            if (hit_sphere<false>(sphere_at<LS>(S, i), o, d, R.a, ia, tmin, R.tmax, lo, hi, t)) {
                 R.tmax = t;
                 R.tmax32 = tmax_f32(t);
                 hi = lim_tmax(t, R.a);
@@ -1329,11 +1330,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LSCENE ?
             S.quadf_lds = W.lds_quadf;
         }
         S.refs_lds = W.lds_refs;
-        S.spheres_lds = W.spheres_f32 ? ~0u : W.lds_spheres;
+        S.spheres_lds = W.spheres_f32 ? (W.bytes_sph64 ? W.lds_sph64 : ~0u) : W.lds_spheres;
         if (W.spheres_f32) {
             // sphere-only: the filter's pair records in LDS; refs are unused (slot = sphere),
             // and the f64 spheres (candidates' exact tests, shading) stay in HBM / L1
             stage_lds(smem + W.lds_spheres, Sg.spair, W.bytes_spheres);
+            if (W.bytes_sph64) stage_lds(smem + W.lds_sph64, Sg.spheres, W.bytes_sph64);
             S.spair_lds = W.lds_spheres;
         } else {
             stage_lds(smem + W.lds_refs, Sg.refs, W.bytes_refs);
@@ -1881,6 +1883,13 @@ static size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
 #define CRT_LDS_BUDGET_KB 40
 #endif
 constexpr size_t kLdsSceneBudget = CRT_LDS_BUDGET_KB * 1024;  // scene + stack per block
+// sphere-only LDS scenes also stage the f64 spheres (pass 2's exact tests, shading) when the block
+// still fits 40 KB: rtow 40.6 KB, 84.7 vs 85.4 ms with them in HBM / L1 (v12; round 1's layout,
+// with even-aligned filter records to make room, had measured the opposite)
+#ifndef CRT_SPH64_LDS
+#define CRT_SPH64_LDS 1
+#endif
+constexpr bool kSph64Lds = CRT_SPH64_LDS != 0;
 constexpr size_t kLdsStackBudget = 32 * 1024 * dev::kBlock / 256;
 
 // Partial-sum budget per launch (bytes): the owned frame is rendered in bands whose partial sums
@@ -2095,7 +2104,11 @@ static int dispatch_render(const crt_scene* s, int device, const crt_camera* cam
         W.lds_spheres = W.lds_refs + W.bytes_refs;
         W.lds_quads = W.lds_spheres + W.bytes_spheres;
         W.lds_quadf = W.lds_quads + W.bytes_quads;
-        W.lds_stack = stack_at(scene_bytes);
+        W.lds_sph64 = W.lds_quadf + W.bytes_quadf;
+        const uint32_t sph64 = static_cast<uint32_t>(s->spheres.size() * sizeof(DevSphere));
+        if (W.spheres_f32 && kSph64Lds && stack_at(scene_bytes + sph64) + stack_bytes + align16(sizeof(dev::CamView)) <= kLdsSceneBudget)
+            W.bytes_sph64 = sph64;
+        W.lds_stack = stack_at(scene_bytes + W.bytes_sph64);
         return launch_render<SE, false, true>(s, device, cam, W, W.lds_stack + stack_bytes, d_rgb, st, count_stats);
     }
     // HBM scene: the top of the (breadth-first) node array goes to LDS as far as it fits beside
