@@ -1304,7 +1304,7 @@ constexpr int kPrioWalk = CRT_PRIO_WALK, kPrioLeaf = CRT_PRIO_LEAF, kPrioShade =
               kPrioInit = CRT_PRIO_INIT;
 template <int P>
 __device__ __forceinline__ void set_prio() {
-    if constexpr (kPrioWalk || kPrioLeaf || kPrioShade || kPrioInit) __builtin_amdgcn_s_setprio(P);
+    if constexpr ((kPrioWalk | kPrioLeaf | kPrioShade | kPrioInit) != 0) __builtin_amdgcn_s_setprio(P);
 }
 // per-round lane counts in the instrumented pass (printed under CRT_DEBUG_COUNTERS); off by default:
 // their atomics shift the instrumented pass's phase timings
