@@ -915,48 +915,66 @@ __device__ __forceinline__ void walk(const SceneView& S, Stack<SE>& st, const do
         // values are monotone in the bounds (near(child) >= near(parent), far(child) <=
         // far(parent)), so the test fails for them at any t_max the culled one failed at.
         // Only node visits are added. The stack stays within depth + 1 levels: it is the same DFS.
-        bool run = true, pend = false;
-        uint32_t pf = 0, pc = 0;
+        // The loop is the wave's (no per-lane exit): a parked lane runs the body again at the
+        // same node and stays parked (`run` is sticky), changing nothing but the dead level
+        // above its stack. The recorded node is `pref` (~0u: none yet; the sentinel when the
+        // lane entered it with no leaf recorded: traversal over), so the loop's exit test is one
+        // compare.
+        bool run = true;
+        uint32_t pref = ~0u;
         do {
-            if (run) {
-                Uvec4 q0, q1;
-                fetch_nodef<TOP, LS>(S, cur, q0, q1);
-                w0 = q1.z;
-                w1 = q1.w;
-                const uint32_t top = *tp;  // speculative pop
-                const float x0 = __builtin_fmaf(__uint_as_float(q0.x), R.inv32[0], -R.oinv32[0]);
-                const float x1 = __builtin_fmaf(__uint_as_float(q0.y), R.inv32[0], -R.oinv32[0]);
-                const float y0 = __builtin_fmaf(__uint_as_float(q0.z), R.inv32[1], -R.oinv32[1]);
-                const float y1 = __builtin_fmaf(__uint_as_float(q0.w), R.inv32[1], -R.oinv32[1]);
-                const float z0 = __builtin_fmaf(__uint_as_float(q1.x), R.inv32[2], -R.oinv32[2]);
-                const float z1 = __builtin_fmaf(__uint_as_float(q1.y), R.inv32[2], -R.oinv32[2]);
-                const float lo = vmax3(vmin(x0, x1), vmin(y0, y1), vmax_s(vmin(z0, z1), tmin32));
-                const float hi = vmin3(vmax(x0, x1), vmax(y0, y1), vmin(vmax(z0, z1), R.tmax32));
-                const float gap = hi - lo;
-                const float th = __builtin_fmaf(vmax_abs(lo, hi), 0x1p-19f, R.marg);
-                bool enter = gap > 0.f;
-                const bool unc = !(fabsf(gap) > th);
-                if (__builtin_expect(__ballot(unc) != 0, 0)) {
-                    if (unc) enter = slab64(node64(S, cur), o, d, tmin, R.tmax);
-                }
-                const bool inner = enter & (w1 < kLeafFlagF);
-                const uint32_t near = w1 | (__builtin_amdgcn_ubfe(R.neg, w0, 1) << kNodeFShift);
-                tp[stride] = static_cast<SE>(near ^ (1u << kNodeFShift));
-                const bool reached = enter ^ inner;  // entered, not interior: a leaf or the sentinel
-                const bool park = reached & (pend | (w1 == kSentinelW1));
-                const bool rec = reached & !park;  // the first leaf: recorded, popped, walk on
-                pf = rec ? w0 : pf;
-                pc = rec ? w1 : pc;
-                pend |= rec;
-                run = !park;
-                cur = inner ? near : (park ? cur : top);
-                tp += inner ? stride : (park ? 0 : -stride);
+            Uvec4 q0, q1;
+            fetch_nodef<TOP, LS>(S, cur, q0, q1);
+            w0 = q1.z;
+            w1 = q1.w;
+            const uint32_t top = *tp;  // speculative pop
+            if (COUNT && run) {
+                if (w1 != kSentinelW1) ctr.nodes++;
+                if (wave_leader()) ctr.it_walk++;
             }
-        } while (__ballot(run & !pend) != 0);
-        // a lane without a recorded leaf parked at the sentinel: traversal over
-        R.state = pend ? kLeaf : kDone;
-        R.first = pf;
-        R.count = pc & ~kLeafFlagF;
+            const float x0 = __builtin_fmaf(__uint_as_float(q0.x), R.inv32[0], -R.oinv32[0]);
+            const float x1 = __builtin_fmaf(__uint_as_float(q0.y), R.inv32[0], -R.oinv32[0]);
+            const float y0 = __builtin_fmaf(__uint_as_float(q0.z), R.inv32[1], -R.oinv32[1]);
+            const float y1 = __builtin_fmaf(__uint_as_float(q0.w), R.inv32[1], -R.oinv32[1]);
+            const float z0 = __builtin_fmaf(__uint_as_float(q1.x), R.inv32[2], -R.oinv32[2]);
+            const float z1 = __builtin_fmaf(__uint_as_float(q1.y), R.inv32[2], -R.oinv32[2]);
+            const float lo = vmax3(vmin(x0, x1), vmin(y0, y1), vmax_s(vmin(z0, z1), tmin32));
+            const float hi = vmin3(vmax(x0, x1), vmax(y0, y1), vmin(vmax(z0, z1), R.tmax32));
+            const float gap = hi - lo;
+            const float th = __builtin_fmaf(vmax_abs(lo, hi), 0x1p-19f, R.marg);
+            bool enter = gap > 0.f;
+            // parked lanes decide again too (the same decision; `run` keeps them parked anyway)
+            const bool unc = !(fabsf(gap) > th);
+            if (__builtin_expect(__ballot(unc) != 0, 0)) {
+                if (COUNT && wave_leader()) ctr.it_slow++;
+                if (unc) {
+                    if (COUNT && run) ctr.slow_nodes++;
+                    enter = slab64(node64(S, cur), o, d, tmin, R.tmax);
+                }
+            }
+            const bool inner = enter & (w1 < kLeafFlagF);
+            const uint32_t near = w1 | (__builtin_amdgcn_ubfe(R.neg, w0, 1) << kNodeFShift);
+            tp[stride] = static_cast<SE>(near ^ (1u << kNodeFShift));
+            const bool reached = enter & !inner;  // a leaf or the sentinel
+            const bool pend = pref != ~0u;
+            const bool rec = run & reached & !pend;  // the first leaf (or the sentinel)
+            const bool park = !run | (reached & (pend | (w1 == kSentinelW1)));
+            pref = rec ? cur : pref;
+            run = !park;
+            const uint32_t nxt = park ? cur : top;
+            cur = inner & !park ? near : nxt;
+            tp += inner & !park ? stride : (park ? 0 : -stride);
+        } while (__ballot(pref == ~0u) != 0);
+        // the recorded node's words (a leaf's primitive range, or the sentinel: traversal over)
+        {
+            Uvec4 q0, q1;
+            fetch_nodef<TOP, LS>(S, pref, q0, q1);
+            w0 = q1.z;
+            w1 = q1.w;
+        }
+        R.state = w1 == kSentinelW1 ? kDone : kLeaf;
+        R.first = w0;
+        R.count = w1 & ~kLeafFlagF;
         R.cur = cur;
         R.sp = static_cast<int32_t>(static_cast<uint32_t>(tp - empty)) / static_cast<int32_t>(st.stride);
         return;
@@ -1343,10 +1361,15 @@ constexpr int kShadeMin = CRT_SHADE_MIN, kPendingMax = CRT_PENDING_MAX;
 constexpr bool kTopTreelet = CRT_TOP_TREELET != 0;
 // speculative walk (walk(): lanes that found their first leaf walk on to the next one); the
 // instrumented pass (COUNT) keeps the plain walk, so its node counts are the reference's
+// (CRT_COUNT_SPEC=1: the instrumented pass walks speculatively too, for phase timings; its node
+// counts then include the speculative visits)
 #ifndef CRT_SPEC_WALK
 #define CRT_SPEC_WALK 1
 #endif
-constexpr bool kSpecWalk = CRT_SPEC_WALK != 0;
+#ifndef CRT_COUNT_SPEC
+#define CRT_COUNT_SPEC 0
+#endif
+constexpr bool kSpecWalk = CRT_SPEC_WALK != 0, kCountSpec = CRT_COUNT_SPEC != 0;
 // Static wave priority per phase (s_setprio 0-3; the SQ issues a ready instruction of the highest
 // priority wave first, then the oldest): the traversal phases are dependency chains (LDS read ->
 // test -> next address), the shade and path-start phases have more independent work to fill in.
@@ -1557,9 +1580,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LSCENE ?
             if (COUNT) cw -= static_cast<uint32_t>(wall_clock64());
             set_prio<kPrioWalk>();
             if (!W.exact_slab && __ballot(R.state == kWalk && (R.neg & kZeroDir)) == 0) {
-                if (R.state == kWalk) walk<SE, COUNT, false, kTopTreelet && !LSCENE, LSCENE, GSTACK, kSpecWalk && !COUNT>(S, st, P.o, P.d, C.t_min, tmin32, R, ctr);
+                if (R.state == kWalk) walk<SE, COUNT, false, kTopTreelet && !LSCENE, LSCENE, GSTACK, kSpecWalk && (!COUNT || kCountSpec)>(S, st, P.o, P.d, C.t_min, tmin32, R, ctr);
             } else {
-                if (R.state == kWalk) walk<SE, COUNT, true, kTopTreelet && !LSCENE, LSCENE, GSTACK, kSpecWalk && !COUNT>(S, st, P.o, P.d, C.t_min, tmin32, R, ctr);
+                if (R.state == kWalk) walk<SE, COUNT, true, kTopTreelet && !LSCENE, LSCENE, GSTACK, kSpecWalk && (!COUNT || kCountSpec)>(S, st, P.o, P.d, C.t_min, tmin32, R, ctr);
             }
             if (COUNT) cw += static_cast<uint32_t>(wall_clock64());
             set_prio<kPrioLeaf>();
