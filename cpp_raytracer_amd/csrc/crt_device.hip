@@ -63,6 +63,8 @@ struct SceneView {
     const uint32_t* quad_mat;
     const DevMaterial* mats;
     const DevQuadF* quadf;       // f32 filter records of the parallelograms (HBM)
+    const DevMaterial* sphere_mrec;  // per-slot material records (shade)
+    const DevMaterial* quad_mrec;
     uint32_t quadf_lds;          // LSCENE kernels: LDS byte offset of the staged copy
     // LSCENE kernels: LDS byte offsets of the staged refs / f64 spheres / parallelograms, read
     // through typed LDS pointers (ds_read, not flat); spheres_lds = ~0u when the spheres stay in HBM
@@ -1231,10 +1233,11 @@ __device__ __forceinline__ bool shade(const SceneView& S, const CamView& C, Path
         acc[2] = acc[2] + P.T[2] * C.bg[2];
         return true;
     }
+    // the slot's material record, loaded first (its address needs only the slot)
+    const DevMaterial& M = (ref & kRefQuad) ? S.quad_mrec[ref & ~kRefQuad] : S.sphere_mrec[ref];
     double p[3], n[3];
     bool front;
-    const uint32_t mi = hit_record<LS>(S, ref, P.o, P.d, t, p, n, front);
-    const DevMaterial& M = S.mats[mi];
+    (void)hit_record<LS>(S, ref, P.o, P.d, t, p, n, front);
     const uint32_t kind = M.kind;
     const bool lam = kind == CRT_LAMBERTIAN, met = kind == CRT_METAL, die = kind == CRT_DIELECTRIC;
     if (!(lam || met || die)) {  // DiffuseLight: emits, never scatters (material.h:248-263)
@@ -1754,7 +1757,7 @@ __global__ __launch_bounds__(kBlock) void hits_kernel(SceneView S, const double*
 
 static dev::SceneView view_of(const DeviceCopy& c) {
     return dev::SceneView{c.nodes, c.fnodes, 0, c.refs, c.spheres, c.spair, 0, c.sphere_mat, c.quads, c.quad_mat,
-                          c.mats, c.quadf, 0};
+                          c.mats, c.quadf, c.sphere_mrec, c.quad_mrec, 0};
 }
 
 int device_count(int* n) {
@@ -1884,7 +1887,12 @@ int device_upload(crt_scene* s, int device) {
     size_t off_qf = align256(off_q + n_q * sizeof(DevQuad));
     size_t off_qm = align256(off_qf + n_q * sizeof(DevQuadF));
     size_t off_m = align256(off_qm + n_q * 4);
-    size_t total = align256(off_m + std::max<size_t>(1, n_m) * sizeof(DevMaterial));
+    size_t off_smr = align256(off_m + std::max<size_t>(1, n_m) * sizeof(DevMaterial));
+    size_t off_qmr = align256(off_smr + n_sp * sizeof(DevMaterial));
+    size_t total = align256(off_qmr + n_q * sizeof(DevMaterial));
+    std::vector<DevMaterial> smrec(n_sp), qmrec(n_q);
+    for (size_t i = 0; i < n_sp; ++i) smrec[i] = s->dmats[s->sphere_mat[i]];
+    for (size_t i = 0; i < n_q; ++i) qmrec[i] = s->dmats[s->quad_mat[i]];
     void* base = nullptr;
     HIP_TRY(hipMalloc(&base, total));
     char* b = static_cast<char*>(base);
@@ -1903,6 +1911,8 @@ int device_upload(crt_scene* s, int device) {
     if (e == hipSuccess) e = up(off_qf, quadf.data(), n_q * sizeof(DevQuadF));
     if (e == hipSuccess) e = up(off_qm, s->quad_mat.data(), n_q * 4);
     if (e == hipSuccess) e = up(off_m, s->dmats.data(), n_m * sizeof(DevMaterial));
+    if (e == hipSuccess) e = up(off_smr, smrec.data(), n_sp * sizeof(DevMaterial));
+    if (e == hipSuccess) e = up(off_qmr, qmrec.data(), n_q * sizeof(DevMaterial));
     if (e != hipSuccess) {
         (void)hipFree(base);
         return fail(CRT_E_HIP, std::string("scene upload: ") + hipGetErrorString(e));
@@ -1922,6 +1932,8 @@ int device_upload(crt_scene* s, int device) {
     c.quads_f32_ok = quads_f32_ok && std::getenv("CRT_F64_QUADS") == nullptr;
     c.quad_mat = reinterpret_cast<uint32_t*>(b + off_qm);
     c.mats = reinterpret_cast<DevMaterial*>(b + off_m);
+    c.sphere_mrec = reinterpret_cast<DevMaterial*>(b + off_smr);
+    c.quad_mrec = reinterpret_cast<DevMaterial*>(b + off_qmr);
     c.valid = true;
     return CRT_OK;
 }

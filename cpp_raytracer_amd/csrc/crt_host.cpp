@@ -1104,7 +1104,8 @@ int crt_scene_info_get(const crt_scene* s, crt_scene_info* info) {
     r.device_bytes = s->dnodes.size() * sizeof(DevNode) + s->refs.size() * 4 +
                      s->spheres.size() * sizeof(DevSphere) + s->sphere_mat.size() * 4 +
                      s->quads.size() * sizeof(DevQuad) + s->quad_mat.size() * 4 +
-                     s->dmats.size() * sizeof(DevMaterial);
+                     s->dmats.size() * sizeof(DevMaterial) +
+                     (s->spheres.size() + s->quads.size()) * sizeof(DevMaterial);  // per-slot copies
     r.build_ms = s->build_ms;
     *info = r;
     return CRT_OK;

@@ -105,6 +105,10 @@ struct DeviceCopy {
     bool quads_f32_ok = false;       // every parallelogram within the filter's range
     uint32_t* quad_mat = nullptr;
     DevMaterial* mats = nullptr;
+    // the material of every sphere / parallelogram slot (the render kernel's shading reads one
+    // record by the hit's slot instead of an index and then the material)
+    DevMaterial* sphere_mrec = nullptr;
+    DevMaterial* quad_mrec = nullptr;
     // per-device scratch reused across renders (partial sums of sample chunks)
     double* partial = nullptr;
     size_t partial_bytes = 0;
