@@ -964,8 +964,8 @@ __device__ __forceinline__ void walk(const SceneView& S, Stack<SE>& st, const do
             pref = rec ? cur : pref;
             run = !park;
             const uint32_t nxt = park ? cur : top;
-            cur = inner & !park ? near : nxt;
-            tp += inner & !park ? stride : (park ? 0 : -stride);
+            cur = (inner & !park) ? near : nxt;
+            tp += (inner & !park) ? stride : (park ? 0 : -stride);
         } while (__ballot(pref == ~0u) != 0);
         // the recorded node's words (a leaf's primitive range, or the sentinel: traversal over)
         {
@@ -1854,30 +1854,12 @@ int device_upload(crt_scene* s, int device) {
         DevSpherePair& last = spair[n_sp - 1];
         last.cx[1] = last.cy[1] = last.cz[1] = last.r2e[1] = 0;
     }
-    // parallelogram filter records (crt_quad_filter.h): f32 v, s1, s2, sn and rounded-up norms
+    // parallelogram filter records (crt_quad_filter.h quad_record)
     std::vector<DevQuadF> quadf(n_q);
     bool quads_f32_ok = true;
     for (size_t i = 0; i < n_q; ++i) {
         const DevQuad& q = s->quads[i];
-        DevQuadF& f = quadf[i];
-        double sn1 = 0, S1 = 0, S2 = 0;
-        for (int k = 0; k < 3; ++k) {
-            f.v[k] = static_cast<float>(q.v[k]);
-            f.s1[k] = static_cast<float>(q.s1[k]);
-            f.s2[k] = static_cast<float>(q.s2[k]);
-            f.sn[k] = static_cast<float>(q.sn[k]);
-            sn1 += std::fabs(q.sn[k]);
-            S1 += std::fabs(q.s1[k]);
-            S2 += std::fabs(q.s2[k]);
-            if (!(std::fabs(q.v[k]) <= kF32QuadMax && std::fabs(q.s1[k]) <= kF32QuadMax &&
-                  std::fabs(q.s2[k]) <= kF32QuadMax))
-                quads_f32_ok = false;
-        }
-        if (!(sn1 >= 0x1p-64 && sn1 <= 0x1p40)) quads_f32_ok = false;
-        f.sn1 = f32_up(sn1 * (1 + 0x1p-20));
-        f.ka = f32_up(sn1 * S2 * (1 + 0x1p-20));
-        f.kb = f32_up(sn1 * S1 * (1 + 0x1p-20));
-        f.pad = 0;
+        if (!quad_record(q.v, q.s1, q.s2, q.sn, quadf[i])) quads_f32_ok = false;
     }
     size_t off_refs = align256(off_fnodes + n_nodes * sizeof(DevNodeF));
     size_t off_sp = align256(off_refs + n_refs * 4);

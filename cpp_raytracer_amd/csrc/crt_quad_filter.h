@@ -7,25 +7,30 @@
 //   w = (o + d t) - v; alpha = sn.(w x s2), beta = sn.(s1 x w); hit iff alpha, beta in [0, 1]
 // (n = unit normal, sn = n / |n|^2 of the ctor, parallelogram.h:269-296). The filter returns false
 // only where that test provably misses, for this t_max and any smaller one: t <= t_min, t >= t_max,
-// alpha or beta outside [0, 1]. It computes the same quantities in f32 from f32-rounded inputs:
+// alpha or beta outside [0, 1]. It computes the same quantities in f32 from f32-rounded inputs,
+// alpha and beta through the triple-product identities alpha = w.(s2 x sn), beta = w.(sn x s1)
+// with g1 = s2 x sn and g2 = sn x s1 precomputed per parallelogram (quad_record):
 //   num' = sn'.(v' - o'), den' = sn'.d', t' = num' * rcp(den')       (sn is parallel to n, so
 //   num'/den' estimates t; the |n| scale cancels)
-//   w' = d' t' - (v' - o'), alpha' = sn'.(w' x s2'), beta' = sn'.(s1' x w')
+//   w' = d' t' - (v' - o'), alpha' = g1'.w', beta' = g2'.w'
 // Error bounds, with u = 2^-24, V = max|v|, O = max|o|, D = max|d|, SN1 = |sn|_1, S1 = |s1|_1,
 // S2 = |s2|_1 (each input rounding, product and sum rounds once, fma once):
 //   |num' - num| <= a' = 6u SN1 (V + O),   |den' - den| <= b' = 5u SN1 D
 //   for |den'| > 2 b':   |num'/den' - t| <= 2 (a' + b' |num'/den'|) / |den'|
 //   rcp (1 ulp) and the product add 3.2u |t'|                      =>  Et
 //   |w'_k - w_k| <= D Et + 3u Mw,  Mw = O + D |t'| + V  (bounds |o|, |d t|, |v|, |w|)
-//   |alpha' - alpha| <= SN1 S2 (D Et + 10u Mw),  |beta' - beta| <= SN1 S1 (D Et + 10u Mw)
+//   g1' = RN32(RN64(s2 x sn)): |g1' - g1|_1 <= u |g1|_1 + 2^-51 S2 SN1, and |g1|_1 <= SN1 S2
+//   (likewise g2 with S1); the three roundings of the dot product add <= 3u(1 + u) |g1'|_1 Mw:
+//   |alpha' - alpha| <= SN1 S2 (D Et + 7.01u Mw),  |beta' - beta| <= SN1 S1 (D Et + 7.01u Mw)
 // The filter uses a = 7u SN1 (V + O), b = 6u SN1 D, Et = 2.5 (a + b|t'|)|rcp| + 4u|t'| and
 // Ea = Ka (1.25 D Et + 14u Mw) with Ka = SN1 S2, Kb = SN1 S1 rounded up on the host (slack >= 15%
-// over every bound: it also covers the rounding of these bound computations and the f64 test's own
-// rounding errors, which are ~2^-29 of the f32 ones), plus absolute floors (2^-80 in a and b, 2^-50
-// in Ea, Eb) for underflow. A rejection needs a TRUE strict comparison against a bound rounded in
-// f32 (x > RN(1 + Ea) implies x > 1 + Ea), so NaN / inf anywhere (0/0, overflowed bounds) keeps
-// the quad a candidate. Valid for |v_k|, |s1_k|, |s2_k|, |o_k| <= 2^30, SN1 in [2^-64, 2^40] per
-// quad (the host sets the scene flag), and D in [2^-30, 2^30] per ray (quad_ray32_ok).
+// over every bound, 2x on the alpha / beta rounding terms: it also covers the rounding of these
+// bound computations and the f64 test's own rounding errors, which are ~2^-29 of the f32 ones),
+// plus absolute floors (2^-80 in a and b, 2^-50 in Ea, Eb) for underflow. A rejection needs a TRUE
+// strict comparison against a bound rounded in f32 (x > RN(1 + Ea) implies x > 1 + Ea), so NaN /
+// inf anywhere (0/0, overflowed bounds) keeps the quad a candidate. Valid for |v_k|, |s1_k|,
+// |s2_k|, |o_k| <= 2^30, SN1 in [2^-64, 2^40] per quad (the host sets the scene flag), and D in
+// [2^-30, 2^30] per ray (quad_ray32_ok).
 #pragma once
 
 #include <cmath>
@@ -39,10 +44,10 @@ namespace crt {
 
 // one f32 parallelogram record (64 bytes, four 16-byte loads)
 struct alignas(16) DevQuadF {
-    float v[3], s1[3], s2[3], sn[3];
+    float v[3], g1[3], g2[3], sn[3];  // g1 = s2 x sn, g2 = sn x s1 (alpha = g1.w, beta = g2.w)
     float sn1;      // |sn|_1, rounded up
     float ka, kb;   // |sn|_1 |s2|_1, |sn|_1 |s1|_1, rounded up
-    float pad;
+    float vmax;     // max_k |v'_k| (exact)
 };
 static_assert(sizeof(DevQuadF) == 64, "f32 quad record");
 constexpr double kF32QuadMax = 0x1p30;
@@ -94,6 +99,33 @@ CRT_HD void quad_ray32(const double o[3], const double d[3], double tmin, double
     L.thi = f32_up(tmax);
 }
 
+// the filter record of a parallelogram (the ctor's v, s1, s2, sn in f64); false when it is outside
+// the filter's range (the scene then decides its parallelograms in f64)
+inline bool quad_record(const double v[3], const double s1[3], const double s2[3], const double sn[3],
+                        DevQuadF& f) {
+    double sn1 = 0, S1 = 0, S2 = 0;
+    bool ok = true;
+    const double g1[3] = {s2[1] * sn[2] - s2[2] * sn[1], s2[2] * sn[0] - s2[0] * sn[2], s2[0] * sn[1] - s2[1] * sn[0]};
+    const double g2[3] = {sn[1] * s1[2] - sn[2] * s1[1], sn[2] * s1[0] - sn[0] * s1[2], sn[0] * s1[1] - sn[1] * s1[0]};
+    float vmax = 0;
+    for (int k = 0; k < 3; ++k) {
+        f.v[k] = static_cast<float>(v[k]);
+        f.g1[k] = static_cast<float>(g1[k]);
+        f.g2[k] = static_cast<float>(g2[k]);
+        f.sn[k] = static_cast<float>(sn[k]);
+        vmax = std::fmax(vmax, std::fabs(f.v[k]));
+        sn1 += std::fabs(sn[k]);
+        S1 += std::fabs(s1[k]);
+        S2 += std::fabs(s2[k]);
+        ok = ok && std::fabs(v[k]) <= kF32QuadMax && std::fabs(s1[k]) <= kF32QuadMax && std::fabs(s2[k]) <= kF32QuadMax;
+    }
+    f.sn1 = f32_up(sn1 * (1 + 0x1p-20));
+    f.ka = f32_up(sn1 * S2 * (1 + 0x1p-20));
+    f.kb = f32_up(sn1 * S1 * (1 + 0x1p-20));
+    f.vmax = vmax;
+    return ok && sn1 >= 0x1p-64 && sn1 <= 0x1p40;
+}
+
 // false only where Parallelogram::hit_by provably misses for t_max (and any smaller t_max);
 // rcp(x) is the hardware reciprocal (within 1 ulp of 1/x)
 template <typename Rcp>
@@ -101,7 +133,7 @@ CRT_HD bool quad_candidate(const DevQuadF& q, const QuadRay32& L, Rcp rcp) {
     const float vx = q.v[0] - L.o[0], vy = q.v[1] - L.o[1], vz = q.v[2] - L.o[2];
     const float num = std::fma(q.sn[2], vz, std::fma(q.sn[1], vy, q.sn[0] * vx));
     const float den = std::fma(q.sn[2], L.d[2], std::fma(q.sn[1], L.d[1], q.sn[0] * L.d[0]));
-    const float V = std::fmax(std::fmax(std::fabs(q.v[0]), std::fabs(q.v[1])), std::fabs(q.v[2]));
+    const float V = q.vmax;
     const float a = std::fma(q.sn1 * (7 * kU), V + L.O, 0x1p-80f);
     const float b = std::fma(q.sn1, L.b6, 0x1p-80f);
     const float r = rcp(den);
@@ -111,15 +143,9 @@ CRT_HD bool quad_candidate(const DevQuadF& q, const QuadRay32& L, Rcp rcp) {
     const bool den_ok = std::fabs(den) > 2 * b;
     const bool t_out = (t + Et < L.tlo) | (t - Et > L.thi);
     const float wx = std::fma(L.d[0], t, -vx), wy = std::fma(L.d[1], t, -vy), wz = std::fma(L.d[2], t, -vz);
-    // alpha = sn . (w x s2), beta = sn . (s1 x w)
-    const float c1x = std::fma(wy, q.s2[2], -(wz * q.s2[1]));
-    const float c1y = std::fma(wz, q.s2[0], -(wx * q.s2[2]));
-    const float c1z = std::fma(wx, q.s2[1], -(wy * q.s2[0]));
-    const float alpha = std::fma(q.sn[2], c1z, std::fma(q.sn[1], c1y, q.sn[0] * c1x));
-    const float c2x = std::fma(q.s1[1], wz, -(q.s1[2] * wy));
-    const float c2y = std::fma(q.s1[2], wx, -(q.s1[0] * wz));
-    const float c2z = std::fma(q.s1[0], wy, -(q.s1[1] * wx));
-    const float beta = std::fma(q.sn[2], c2z, std::fma(q.sn[1], c2y, q.sn[0] * c2x));
+    // alpha = sn . (w x s2) = w . g1, beta = sn . (s1 x w) = w . g2
+    const float alpha = std::fma(q.g1[2], wz, std::fma(q.g1[1], wy, q.g1[0] * wx));
+    const float beta = std::fma(q.g2[2], wz, std::fma(q.g2[1], wy, q.g2[0] * wx));
     const float Mw = std::fma(L.D, at, L.O + V);
     const float base = std::fma(L.D, Et * 1.25f, Mw * (14 * kU));
     const float Ea = std::fma(q.ka, base, 0x1p-50f), Eb = std::fma(q.kb, base, 0x1p-50f);

@@ -70,27 +70,8 @@ static bool exact(const Quad& q, const double o[3], const double d[3], double tm
     return 0 <= alpha && alpha <= 1 && 0 <= beta && beta <= 1;
 }
 
-// the host side of the record (crt_device.hip device_upload)
-static bool record(const Quad& q, DevQuadF& f) {
-    double sn1 = 0, S1 = 0, S2 = 0;
-    bool ok = true;
-    for (int k = 0; k < 3; ++k) {
-        f.v[k] = static_cast<float>(q.v[k]);
-        f.s1[k] = static_cast<float>(q.s1[k]);
-        f.s2[k] = static_cast<float>(q.s2[k]);
-        f.sn[k] = static_cast<float>(q.sn[k]);
-        sn1 += std::fabs(q.sn[k]);
-        S1 += std::fabs(q.s1[k]);
-        S2 += std::fabs(q.s2[k]);
-        ok = ok && std::fabs(q.v[k]) <= crt::kF32QuadMax && std::fabs(q.s1[k]) <= crt::kF32QuadMax &&
-             std::fabs(q.s2[k]) <= crt::kF32QuadMax;
-    }
-    f.sn1 = crt::f32_up(sn1 * (1 + 0x1p-20));
-    f.ka = crt::f32_up(sn1 * S2 * (1 + 0x1p-20));
-    f.kb = crt::f32_up(sn1 * S1 * (1 + 0x1p-20));
-    f.pad = 0;
-    return ok && sn1 >= 0x1p-64 && sn1 <= 0x1p40;
-}
+// the host side of the record (crt_quad_filter.h quad_record, as crt_device.hip device_upload)
+static bool record(const Quad& q, DevQuadF& f) { return crt::quad_record(q.v, q.s1, q.s2, q.sn, f); }
 
 static float rcp_adversarial(float x) {
     float r = 1.0f / x;
