@@ -1,6 +1,7 @@
 """Per-rank render time of the config-2 frame when its rows are dealt over N ranks (4-row blocks),
-measured on one GPU by rendering rank 0's share: estimates strong-scaling efficiency
-T(1) / (N * T_rank0(N)) without N GPUs. usage: python tools/tile_timing.py [steps]"""
+measured on one GPU by rendering each rank's share alone: estimates strong-scaling efficiency
+T(1) / (N * max_r T_r(N)) without N GPUs. usage: python tools/tile_timing.py [steps] [all]
+(all: every rank of every N; default: ranks 0 and N - 1)"""
 import os
 import sys
 import time
@@ -12,6 +13,7 @@ import cpp_raytracer_amd as crt  # noqa: E402
 from cpp_raytracer_amd import Tiling, camera_with  # noqa: E402
 
 steps = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+all_ranks = len(sys.argv) > 2 and sys.argv[2] == "all"
 d = crt.SceneData.named("rtow_final", 42)
 d.camera = camera_with(d.camera, image_w=1200, image_h=800, samples_per_pixel=500, max_depth=50)
 s = crt.GpuScene(d)
@@ -22,7 +24,8 @@ st = torch.cuda.current_stream()
 t1 = None
 for n in (1, 2, 4, 8):
     worst = 0.0
-    for r in (0, n - 1):
+    per = []
+    for r in (range(n) if all_ranks else (0, n - 1)):
         tl = Tiling(4, n, r, 0)
         s.render_async(0, cam, frame.data_ptr(), st.cuda_stream, tl)
         torch.cuda.synchronize()
@@ -30,7 +33,9 @@ for n in (1, 2, 4, 8):
         for _ in range(steps):
             s.render_async(0, cam, frame.data_ptr(), st.cuda_stream, tl)
         torch.cuda.synchronize()
-        worst = max(worst, (time.perf_counter() - t0) / steps)
+        per.append((time.perf_counter() - t0) / steps)
+        worst = max(worst, per[-1])
     if n == 1:
         t1 = worst
-    print(f"N={n}: slowest rank {worst * 1e3:.1f} ms, est. efficiency {t1 / (n * worst):.3f}", flush=True)
+    print(f"N={n}: slowest rank {worst * 1e3:.1f} ms, est. efficiency {t1 / (n * worst):.3f}"
+          + (f" (ranks: {' '.join(f'{x * 1e3:.2f}' for x in per)} ms)" if all_ranks else ""), flush=True)
