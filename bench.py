@@ -261,6 +261,9 @@ def main():
                      "peak_tflops": FP64_VECTOR_PEAK_TFLOPS, "rays_per_sample": round(rays_per_sample, 4),
                      "nodes_per_ray": round(cnt.nodes_visited / max(1, cnt.rays), 3),
                      "prim_tests_per_ray": round((cnt.sphere_tests + cnt.parallelogram_tests) / max(1, cnt.rays), 3)},
+            # per-phase shares and lane utilization of the instrumented pass, which walks like
+            # the reference (no speculative walk) so that its node counts are the byte basis
+            "instrumented_pass": "plain walk (reference node-test counts); timed kernel walks speculatively",
             "wave_time_share": {k: round(getattr(cnt, "ticks_" + k) / max(1, cnt.ticks_total), 4)
                                 for k in ("walk", "leaf", "shade", "tail")},
             "lane_utilization": {
