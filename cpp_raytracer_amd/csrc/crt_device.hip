@@ -45,6 +45,11 @@ constexpr int kBlock = CRT_BLOCK;
 #define CRT_TILE_W 16
 #endif
 constexpr uint32_t kTileW = CRT_TILE_W, kTileH = 64 / CRT_TILE_W;
+// the speculative walk's parked lanes leave the loop through the exec mask (1) or re-run its body
+// at their node (0)
+#ifndef CRT_SPEC_MASKED
+#define CRT_SPEC_MASKED 1
+#endif
 constexpr double kScale = 1 / static_cast<double>(4294967295u - 1);  // rand_util.h:110-112
 
 typedef double Dvec2 __attribute__((ext_vector_type(2)));
@@ -917,6 +922,62 @@ __device__ __forceinline__ void walk(const SceneView& S, Stack<SE>& st, const do
         // values are monotone in the bounds (near(child) >= near(parent), far(child) <=
         // far(parent)), so the test fails for them at any t_max the culled one failed at.
         // Only node visits are added. The stack stays within depth + 1 levels: it is the same DFS.
+#if CRT_SPEC_MASKED
+        // The loop is the wave's; parked lanes leave it through the exec mask (`run`). A lane
+        // parks by popping like at any entered leaf and remembering the node (`pcur`); after the
+        // loop its pop is undone. The recorded node is `pref` (~0u: none yet; the sentinel when
+        // the lane entered it with no leaf recorded: traversal over), so the loop's exit test is
+        // one compare.
+        bool run = true, nopend = true;
+        uint32_t pref = ~0u, pcur = 0;
+        do {
+            if (run) {
+                Uvec4 q0, q1;
+                fetch_nodef<TOP, LS>(S, cur, q0, q1);
+                w0 = q1.z;
+                w1 = q1.w;
+                const uint32_t top = *tp;  // speculative pop
+                if (COUNT) {
+                    if (w1 != kSentinelW1) ctr.nodes++;
+                    if (wave_leader()) ctr.it_walk++;
+                }
+                const float x0 = __builtin_fmaf(__uint_as_float(q0.x), R.inv32[0], -R.oinv32[0]);
+                const float x1 = __builtin_fmaf(__uint_as_float(q0.y), R.inv32[0], -R.oinv32[0]);
+                const float y0 = __builtin_fmaf(__uint_as_float(q0.z), R.inv32[1], -R.oinv32[1]);
+                const float y1 = __builtin_fmaf(__uint_as_float(q0.w), R.inv32[1], -R.oinv32[1]);
+                const float z0 = __builtin_fmaf(__uint_as_float(q1.x), R.inv32[2], -R.oinv32[2]);
+                const float z1 = __builtin_fmaf(__uint_as_float(q1.y), R.inv32[2], -R.oinv32[2]);
+                const float lo = vmax3(vmin(x0, x1), vmin(y0, y1), vmax_s(vmin(z0, z1), tmin32));
+                const float hi = vmin3(vmax(x0, x1), vmax(y0, y1), vmin(vmax(z0, z1), R.tmax32));
+                const float gap = hi - lo;
+                const float th = __builtin_fmaf(vmax_abs(lo, hi), 0x1p-19f, R.marg);
+                bool enter = gap > 0.f;
+                const bool unc = !(fabsf(gap) > th);
+                if (__builtin_expect(__ballot(unc) != 0, 0)) {
+                    if (COUNT && wave_leader()) ctr.it_slow++;
+                    if (unc) {
+                        if (COUNT) ctr.slow_nodes++;
+                        enter = slab64(node64(S, cur), o, d, tmin, R.tmax);
+                    }
+                }
+                const bool inner = enter & (w1 < kLeafFlagF);
+                const uint32_t near = w1 | (__builtin_amdgcn_ubfe(R.neg, w0, 1) << kNodeFShift);
+                tp[stride] = static_cast<SE>(near ^ (1u << kNodeFShift));
+                const bool reached = enter & !inner;  // a leaf or the sentinel
+                const bool park = reached & (!nopend | (w1 == kSentinelW1));
+                pref = (reached & nopend) ? cur : pref;  // the first leaf (or the sentinel)
+                pcur = park ? cur : pcur;
+                run = !park;
+                cur = inner ? near : top;
+                tp += inner ? stride : -stride;
+            }
+            nopend = pref == ~0u;
+        } while (__ballot(nopend) != 0);
+        if (!run) {  // parked: back at the node, its pop undone
+            cur = pcur;
+            tp += stride;
+        }
+#else
         // The loop is the wave's (no per-lane exit): a parked lane runs the body again at the
         // same node and stays parked (`run` is sticky), changing nothing but the dead level
         // above its stack. The recorded node is `pref` (~0u: none yet; the sentinel when the
@@ -967,6 +1028,7 @@ __device__ __forceinline__ void walk(const SceneView& S, Stack<SE>& st, const do
             cur = (inner & !park) ? near : nxt;
             tp += (inner & !park) ? stride : (park ? 0 : -stride);
         } while (__ballot(pref == ~0u) != 0);
+#endif
         // the recorded node's words (a leaf's primitive range, or the sentinel: traversal over)
         {
             Uvec4 q0, q1;
