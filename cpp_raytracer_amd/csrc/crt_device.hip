@@ -514,8 +514,11 @@ __device__ __forceinline__ T lds_rec(uint32_t off) {
 __device__ __forceinline__ uint32_t lds_u32(uint32_t off) {
     return *(__attribute__((address_space(3))) const uint32_t*)static_cast<uintptr_t>(off);
 }
-// the verdicts of the record's two spheres: bit 1 = first, bit 0 = second (1 = candidate)
-__device__ __forceinline__ uint32_t sphere_pair_candidates(const DevSpherePair& sp, const LeafRay32& L) {
+// the verdicts of the record's two spheres shifted into cand: bit 1 = first, bit 0 = second
+// (1 = candidate); cand = cand + cand + verdict by v_addc_co_u32 with the compare's VCC as the
+// carry (written out: the compiler turns the C form into a shift, two selects and an or); the
+// s_nop 1 is the VALU-writes-VCC -> VALU-reads-VCC hazard the compiler pads the same way
+__device__ __forceinline__ uint32_t sphere_pair_candidates(uint32_t cand, const DevSpherePair& sp, const LeafRay32& L) {
     const F2 cx = {sp.cx[0], sp.cx[1]}, cy = {sp.cy[0], sp.cy[1]}, cz = {sp.cz[0], sp.cz[1]};
     const F2 r2e = {sp.r2e[0], sp.r2e[1]};
     const F2 xx = sub_pL(L.oxy, cx), xy = sub_pH(L.oxy, cy), xz = sub_pL(L.ozdx, cz);
@@ -526,7 +529,11 @@ __device__ __forceinline__ uint32_t sphere_pair_candidates(const DevSpherePair& 
     const F2 y = nsub_pL(b, L.hilo), w = add_bH(b, L.hilo);
     const float m0 = vmax3_0(vmul_abs(y.x, y.x), vmul_abs(w.x, w.x));
     const float m1 = vmax3_0(vmul_abs(y.y, y.y), vmul_abs(w.y, w.y));
-    return (static_cast<uint32_t>(!(m0 > D.x)) << 1) | static_cast<uint32_t>(!(m1 > D.y));
+    asm volatile("v_cmp_ngt_f32 vcc, %1, %2\n\ts_nop 1\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc"
+                 : "+v"(cand) : "v"(m0), "v"(D.x) : "vcc");
+    asm volatile("v_cmp_ngt_f32 vcc, %1, %2\n\ts_nop 1\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc"
+                 : "+v"(cand) : "v"(m1), "v"(D.y) : "vcc");
+    return cand;
 }
 
 // Parallelogram::hit_by (parallelogram.h:177-240)
@@ -1126,7 +1133,7 @@ __device__ __forceinline__ void leaf_step(const SceneView& S, Stack<SE>& st, con
             }
             const DevSpherePair rec = LS ? pair_at((LdsPair*)static_cast<uintptr_t>(S.spair_lds + ((range.x + i) << 5)))
                                          : pair_at((GlobalPair*)(S.spair + range.x + i));
-            cand = (cand << 2) | sphere_pair_candidates(rec, L);
+            cand = sphere_pair_candidates(cand, rec, L);
         }
         cand &= ~(range.y & 1u);  // an odd count's last verdict is the slot after the leaf
         while (cand) {
