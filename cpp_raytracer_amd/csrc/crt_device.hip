@@ -189,12 +189,19 @@ __device__ __forceinline__ uint32_t sample_seed(uint32_t base, uint32_t pixel, u
 // Vec3D::random_unit_vector (vec3d.h:64-75): rejection in the cube, then * (1 / |v|)
 __device__ __forceinline__ void random_unit_vector(uint32_t& s, double& x, double& y, double& z) {
     double m2;
+#if CRT_ABLATE_RUV  // timing experiment only (wrong results): one candidate, no rejection loop
+    x = rnd(s, -1, 1);
+    y = rnd(s, -1, 1);
+    z = rnd(s, -1, 1);
+    m2 = x * x + y * y + z * z;
+#else
     do {
         x = rnd(s, -1, 1);
         y = rnd(s, -1, 1);
         z = rnd(s, -1, 1);
         m2 = x * x + y * y + z * z;
     } while (!(m2 < 1));
+#endif
     double inv = 1 / sqrt(x * x + y * y + z * z);
     x = x * inv;
     y = y * inv;
@@ -570,10 +577,12 @@ __device__ __forceinline__ DevSphere sphere_at(const SceneView& S, uint32_t i) {
 }
 
 // Resolve the hit record (hittable.h:46-71): hit point ray(t), outward normal, front face.
-template <bool LS>
+// IR: the sphere's 1/r comes in as ir (shade: the slot's material record holds RN(1/r), the
+// same value the division gives); otherwise it is divided here.
+template <bool LS, bool IR = false>
 __device__ __forceinline__ uint32_t hit_record(const SceneView& S, uint32_t ref, const double o[3],
                                                const double d[3], double t, double p[3],
-                                               double nrm[3], bool& front) {
+                                               double nrm[3], bool& front, double ir_in = 0) {
     p[0] = o[0] + d[0] * t;
     p[1] = o[1] + d[1] * t;
     p[2] = o[2] + d[2] * t;
@@ -590,7 +599,7 @@ __device__ __forceinline__ uint32_t hit_record(const SceneView& S, uint32_t ref,
         m = S.quad_mat[ref & ~kRefQuad];
     } else {
         const auto normal = [&](const DevSphere& sp) {
-            const double ir = 1 / sp.r;  // (hit_point - center) / radius
+            const double ir = IR ? ir_in : 1 / sp.r;  // (hit_point - center) / radius
             nx = (p[0] - sp.c[0]) * ir;
             ny = (p[1] - sp.c[1]) * ir;
             nz = (p[2] - sp.c[2]) * ir;
@@ -1263,10 +1272,15 @@ __device__ __forceinline__ void start_path(const CamView& C, uint32_t row, uint3
         P.o[0] = C.o[0]; P.o[1] = C.o[1]; P.o[2] = C.o[2];
     } else {  // random_point_in_defocus_disk (camera.h:160-168, vec3d.h:79-85)
         double vx, vy;
+#if CRT_ABLATE_DISK  // timing experiment only (wrong results): one candidate
+        vx = rnd(rng, -1, 1);
+        vy = rnd(rng, -1, 1);
+#else
         do {
             vx = rnd(rng, -1, 1);
             vy = rnd(rng, -1, 1);
         } while (!(vx * vx + vy * vy + 0.0 * 0.0 < 1));
+#endif
         P.o[0] = (C.o[0] + C.ddx[0] * vx) + C.ddy[0] * vy;
         P.o[1] = (C.o[1] + C.ddx[1] * vx) + C.ddy[1] * vy;
         P.o[2] = (C.o[2] + C.ddx[2] * vx) + C.ddy[2] * vy;
@@ -1306,7 +1320,7 @@ __device__ __forceinline__ bool shade(const SceneView& S, const CamView& C, Path
     const DevMaterial& M = (ref & kRefQuad) ? S.quad_mrec[ref & ~kRefQuad] : S.sphere_mrec[ref];
     double p[3], n[3];
     bool front;
-    (void)hit_record<LS>(S, ref, P.o, P.d, t, p, n, front);
+    (void)hit_record<LS, true>(S, ref, P.o, P.d, t, p, n, front, M.emit[0]);
     const uint32_t kind = M.kind;
     const bool lam = kind == CRT_LAMBERTIAN, met = kind == CRT_METAL, die = kind == CRT_DIELECTRIC;
     if (!(lam || met || die)) {  // DiffuseLight: emits, never scatters (material.h:248-263)
@@ -1331,14 +1345,13 @@ __device__ __forceinline__ bool shade(const SceneView& S, const CamView& C, Path
     bool reflect = met;
     double cosv = 0, ratio = 0;
     if (die) {  // material.h:185-218, vec3d.h:168-200
-        ratio = front ? 1. / M.param : M.param / 1.;
+        ratio = front ? M.color[0] : M.param;  // 1. / ri, ri / 1. (precomputed: upload)
         cosv = fmin((-ux0) * n[0] + (-uy0) * n[1] + (-uz0) * n[2], 1.);
         const double sinv = sqrt(1 - cosv * cosv);
         if (ratio * sinv > 1) {
             reflect = true;  // total internal reflection, no draw
         } else {
-            double r0 = (1 - ratio) / (1 + ratio);
-            r0 = r0 * r0;
+            const double r0 = front ? M.color[1] : M.color[2];  // reflectance's r0 (upload)
             const double refl = r0 + (1 - r0) * pow5(1 - cosv);
             reflect = rnd(P.rng, 0, 1) < refl;
         }
@@ -1942,8 +1955,31 @@ int device_upload(crt_scene* s, int device) {
     size_t off_qmr = align256(off_smr + n_sp * sizeof(DevMaterial));
     size_t total = align256(off_qmr + n_q * sizeof(DevMaterial));
     std::vector<DevMaterial> smrec(n_sp), qmrec(n_q);
-    for (size_t i = 0; i < n_sp; ++i) smrec[i] = s->dmats[s->sphere_mat[i]];
-    for (size_t i = 0; i < n_q; ++i) qmrec[i] = s->dmats[s->quad_mat[i]];
+    // Shading constants precomputed per slot, with the reference's own operations (IEEE f64, no
+    // contraction), so shade reads the values its divisions would give:
+    //   emit[0] of a non-emitting sphere slot = 1 / r (the normal's (p - c) / r, vec3d.h:34);
+    //   a Dielectric's colour (unused: attenuation 1) = the front-face ratio 1. / ri
+    //   (material.h:191) and reflectance's r0 (material.h:178-179) for the front and back ratio.
+    const auto shading_consts = [](DevMaterial& m, const DevSphere* sp) {
+        if (m.kind == CRT_DIELECTRIC) {
+            const auto r0 = [](double ratio) {
+                double r = (1 - ratio) / (1 + ratio);
+                return r * r;
+            };
+            m.color[0] = 1. / m.param;
+            m.color[1] = r0(1. / m.param);
+            m.color[2] = r0(m.param / 1.);
+        }
+        if (sp && m.kind != CRT_DIFFUSE_LIGHT) m.emit[0] = 1 / sp->r;
+    };
+    for (size_t i = 0; i < n_sp; ++i) {
+        smrec[i] = s->dmats[s->sphere_mat[i]];
+        shading_consts(smrec[i], &s->spheres[i]);
+    }
+    for (size_t i = 0; i < n_q; ++i) {
+        qmrec[i] = s->dmats[s->quad_mat[i]];
+        shading_consts(qmrec[i], nullptr);
+    }
     void* base = nullptr;
     HIP_TRY(hipMalloc(&base, total));
     char* b = static_cast<char*>(base);

@@ -83,6 +83,8 @@ struct alignas(16) DevMaterial {
     double param;
     double emit[3];     // DiffuseLight::emit() = intensity * colour (material.h:261-263), else 0
 };
+// The render kernel's per-slot copies (device_upload) also carry shading constants: emit[0] of a
+// non-emitting sphere slot = 1 / r, a Dielectric's colour = (1. / ri, r0 front, r0 back).
 
 // Primitive reference per BVH slot: high bit = parallelogram, low 31 bits = index into the
 // kind's array. Spheres/quads are stored in slot order, so for a sphere-only scene ref == slot.
