@@ -71,6 +71,7 @@ struct SceneView {
     const DevMaterial* sphere_mrec;  // per-slot material records (shade)
     const DevMaterial* quad_mrec;
     uint32_t quadf_lds;          // LSCENE kernels: LDS byte offset of the staged copy
+    const DevQuadBox* quadbox;   // flat boxes of axis-aligned parallelograms (HBM)
     // LSCENE kernels: LDS byte offsets of the staged refs / f64 spheres / parallelograms, read
     // through typed LDS pointers (ds_read, not flat); spheres_lds = ~0u when the spheres stay in HBM
     uint32_t refs_lds, spheres_lds, quads_lds;
@@ -120,6 +121,7 @@ struct Work {
     uint32_t f32_ok;        // node bounds fit the f32 walk's error analysis (else f64 decides)
     uint32_t spheres_f32;   // sphere-only scene within the f32 filter's range (two-pass leaves)
     uint32_t quads_f32;     // parallelogram-only scene within its f32 filter's range (two-pass leaves)
+    uint32_t quads_flat;    // ... and every parallelogram axis-aligned: pass 1 is the flat-box node test
     float tmin32;           // RN32(camera t_min)
 };
 
@@ -1115,8 +1117,8 @@ __device__ __forceinline__ void walk(const SceneView& S, Stack<SE>& st, const do
 // sphere is loaded while the current one is tested.
 template <typename SE, bool COUNT, bool TOP, bool LS>
 __device__ __forceinline__ void leaf_step(const SceneView& S, Stack<SE>& st, const double o[3],
-                                          const double d[3], double tmin, bool sphere_only, bool pairs,
-                                          bool qfilter, Trav& R, LaneCounters& ctr) {
+                                          const double d[3], double tmin, float tmin32, bool sphere_only, bool pairs,
+                                          bool qfilter, bool qflat, Trav& R, LaneCounters& ctr) {
     const uint2 range = make_uint2(R.first, R.count);  // index, count
     const uint32_t end = range.x + range.y;
     const double ia = recip_a(R.a), lo = lim_tmin(tmin, R.a);
@@ -1160,6 +1162,45 @@ __device__ __forceinline__ void leaf_step(const SceneView& S, Stack<SE>& st, con
                 R.tmax32 = tmax_f32(t);
                 hi = lim_tmax(t, R.a);
                 R.ref = i;
+                R.found = true;
+            }
+        }
+    } else if (LS && qfilter && qflat && range.y <= 32) {
+        // axis-aligned parallelograms (every Box face, the Cornell walls): pass 1 is the walk's
+        // f32 node test on each one's flat box (crt_quad_filter.h: a rejection is a proven miss of
+        // the reference's Parallelogram::hit_by for this t_max and any smaller one); rays outside
+        // the walk's range have marg = inf and keep every parallelogram. Pass 2 as below.
+        uint32_t cand = 0;
+        for (uint32_t i = 0; i < range.y; ++i) {
+            if (COUNT) {
+                ctr.quad_tests++;
+                if (wave_leader()) ctr.it_leaf++;
+            }
+            LdsNodeF* p = (LdsNodeF*)static_cast<uintptr_t>(S.quadf_lds + ((range.x + i) << 5));
+            const Uvec4 q0 = p->q0, q1 = p->q1;
+            const float x0 = __builtin_fmaf(__uint_as_float(q0.x), R.inv32[0], -R.oinv32[0]);
+            const float x1 = __builtin_fmaf(__uint_as_float(q0.y), R.inv32[0], -R.oinv32[0]);
+            const float y0 = __builtin_fmaf(__uint_as_float(q0.z), R.inv32[1], -R.oinv32[1]);
+            const float y1 = __builtin_fmaf(__uint_as_float(q0.w), R.inv32[1], -R.oinv32[1]);
+            const float z0 = __builtin_fmaf(__uint_as_float(q1.x), R.inv32[2], -R.oinv32[2]);
+            const float z1 = __builtin_fmaf(__uint_as_float(q1.y), R.inv32[2], -R.oinv32[2]);
+            const float lo = vmax3(vmin(x0, x1), vmin(y0, y1), vmax_s(vmin(z0, z1), tmin32));
+            const float hi = vmin3(vmax(x0, x1), vmax(y0, y1), vmin(vmax(z0, z1), R.tmax32));
+            const float th = __builtin_fmaf(vmax_abs(lo, hi), 0x1p-19f, R.marg);
+            cand |= static_cast<uint32_t>(!(hi - lo < -th)) << i;
+        }
+        while (cand) {
+            if (COUNT) {
+                ctr.cand++;
+                if (wave_leader()) ctr.it_cand++;
+            }
+            const uint32_t i = range.x + static_cast<uint32_t>(__builtin_ctz(cand));
+            cand &= cand - 1;
+            double t;
+            if (hit_quad(lds_rec<DevQuad>(S.quads_lds + (i << 7)), o, d, tmin, R.tmax, t)) {
+                R.tmax = t;
+                R.tmax32 = tmax_f32(t);
+                R.ref = kRefQuad | i;
                 R.found = true;
             }
         }
@@ -1486,7 +1527,9 @@ __device__ __forceinline__ void set_prio() {
 #endif
 constexpr bool kRoundCounters = CRT_ROUND_COUNTERS != 0;
 
-template <typename SE, bool GSTACK, bool LSCENE, bool COUNT>
+// QF: the instance has the parallelogram filters' leaf passes (sphere-only scenes launch the
+// instance without them: their code is not in the kernel at all)
+template <typename SE, bool GSTACK, bool LSCENE, bool COUNT, bool QF>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LSCENE ? CRT_WAVES_PER_EU_LDS : CRT_WAVES_PER_EU, 8))) void render_kernel(
     SceneView Sg, CamView C, Work W, double* __restrict__ partial, SE* __restrict__ gstack,
     Counters* __restrict__ counters) {
@@ -1498,8 +1541,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LSCENE ?
         stage_lds(smem + W.lds_quads, Sg.quads, W.bytes_quads);
         S.quads = reinterpret_cast<const DevQuad*>(smem + W.lds_quads);
         S.quads_lds = W.lds_quads;
-        if (W.quads_f32) {  // the parallelogram filter's records
-            stage_lds(smem + W.lds_quadf, Sg.quadf, W.bytes_quadf);
+        if (W.quads_f32) {  // the parallelogram filter's records (flat boxes when axis-aligned)
+            stage_lds(smem + W.lds_quadf, W.quads_flat ? static_cast<const void*>(Sg.quadbox) : Sg.quadf, W.bytes_quadf);
             S.quadf_lds = W.lds_quadf;
         }
         S.refs_lds = W.lds_refs;
@@ -1676,7 +1719,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LSCENE ?
                 if (wave_leader()) atomicAdd(&counters->round_leaves, nl);
             }
             if (COUNT) cl -= static_cast<uint32_t>(wall_clock64());
-            if (R.state == kLeaf) leaf_step<SE, COUNT, kTopTreelet && !LSCENE, LSCENE>(S, st, P.o, P.d, C.t_min, W.sphere_only != 0, W.spheres_f32 != 0, W.quads_f32 != 0, R, ctr);
+            if (R.state == kLeaf) leaf_step<SE, COUNT, kTopTreelet && !LSCENE, LSCENE>(S, st, P.o, P.d, C.t_min, tmin32, W.sphere_only != 0, W.spheres_f32 != 0, QF && W.quads_f32 != 0, QF && W.quads_flat != 0, R, ctr);
             if (COUNT) cl += static_cast<uint32_t>(wall_clock64());
             const uint64_t pending = __ballot(R.state == kWalk);
             const uint64_t finished = __ballot(R.state == kDone);
@@ -1839,7 +1882,7 @@ __global__ __launch_bounds__(kBlock) void hits_kernel(SceneView S, const double*
 
 static dev::SceneView view_of(const DeviceCopy& c) {
     return dev::SceneView{c.nodes, c.fnodes, 0, c.refs, c.spheres, c.spair, 0, c.sphere_mat, c.quads, c.quad_mat,
-                          c.mats, c.quadf, c.sphere_mrec, c.quad_mrec, 0};
+                          c.mats, c.quadf, c.sphere_mrec, c.quad_mrec, 0, c.quadbox};
 }
 
 int device_count(int* n) {
@@ -1938,10 +1981,12 @@ int device_upload(crt_scene* s, int device) {
     }
     // parallelogram filter records (crt_quad_filter.h quad_record)
     std::vector<DevQuadF> quadf(n_q);
-    bool quads_f32_ok = true;
+    std::vector<DevQuadBox> quadbox(n_q);
+    bool quads_f32_ok = true, quads_flat_ok = true;
     for (size_t i = 0; i < n_q; ++i) {
         const DevQuad& q = s->quads[i];
         if (!quad_record(q.v, q.s1, q.s2, q.sn, quadf[i])) quads_f32_ok = false;
+        if (!quad_flat_box(q.v, q.s1, q.s2, quadbox[i])) quads_flat_ok = false;
     }
     size_t off_refs = align256(off_fnodes + n_nodes * sizeof(DevNodeF));
     size_t off_sp = align256(off_refs + n_refs * 4);
@@ -1949,7 +1994,8 @@ int device_upload(crt_scene* s, int device) {
     size_t off_spm = align256(off_spp + n_sp * sizeof(DevSpherePair));
     size_t off_q = align256(off_spm + n_sp * 4);
     size_t off_qf = align256(off_q + n_q * sizeof(DevQuad));
-    size_t off_qm = align256(off_qf + n_q * sizeof(DevQuadF));
+    size_t off_qb = align256(off_qf + n_q * sizeof(DevQuadF));
+    size_t off_qm = align256(off_qb + n_q * sizeof(DevQuadBox));
     size_t off_m = align256(off_qm + n_q * 4);
     size_t off_smr = align256(off_m + std::max<size_t>(1, n_m) * sizeof(DevMaterial));
     size_t off_qmr = align256(off_smr + n_sp * sizeof(DevMaterial));
@@ -1996,6 +2042,7 @@ int device_upload(crt_scene* s, int device) {
     if (e == hipSuccess) e = up(off_spm, s->sphere_mat.data(), n_sp * 4);
     if (e == hipSuccess) e = up(off_q, s->quads.data(), n_q * sizeof(DevQuad));
     if (e == hipSuccess) e = up(off_qf, quadf.data(), n_q * sizeof(DevQuadF));
+    if (e == hipSuccess) e = up(off_qb, quadbox.data(), n_q * sizeof(DevQuadBox));
     if (e == hipSuccess) e = up(off_qm, s->quad_mat.data(), n_q * 4);
     if (e == hipSuccess) e = up(off_m, s->dmats.data(), n_m * sizeof(DevMaterial));
     if (e == hipSuccess) e = up(off_smr, smrec.data(), n_sp * sizeof(DevMaterial));
@@ -2017,6 +2064,9 @@ int device_upload(crt_scene* s, int device) {
     c.quads = reinterpret_cast<DevQuad*>(b + off_q);
     c.quadf = reinterpret_cast<DevQuadF*>(b + off_qf);
     c.quads_f32_ok = quads_f32_ok && std::getenv("CRT_F64_QUADS") == nullptr;
+    c.quadbox = reinterpret_cast<DevQuadBox*>(b + off_qb);
+    // CRT_GENERIC_QUADS=1: the generic parallelogram filter even for axis-aligned ones
+    c.quads_flat_ok = quads_flat_ok && std::getenv("CRT_GENERIC_QUADS") == nullptr;
     c.quad_mat = reinterpret_cast<uint32_t*>(b + off_qm);
     c.mats = reinterpret_cast<DevMaterial*>(b + off_m);
     c.sphere_mrec = reinterpret_cast<DevMaterial*>(b + off_smr);
@@ -2088,7 +2138,7 @@ static size_t partial_budget() {
     return size_t{4} << 30;
 }
 
-template <typename SE, bool GSTACK, bool LSCENE>
+template <typename SE, bool GSTACK, bool LSCENE, bool QF>
 static int launch_render(const crt_scene* s, int device, const crt_camera* cam, const dev::Work& w0,
                          size_t lds, double* d_rgb, hipStream_t stream, crt_render_stats* count_stats) {
     const DeviceCopy& c = s->dev[device];
@@ -2126,7 +2176,7 @@ static int launch_render(const crt_scene* s, int device, const crt_camera* cam, 
     int cus = 0, per_cu = 0;
     HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
     HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &per_cu, reinterpret_cast<const void*>(dev::render_kernel<SE, GSTACK, LSCENE, false>), dev::kBlock, lds));
+        &per_cu, reinterpret_cast<const void*>(dev::render_kernel<SE, GSTACK, LSCENE, false, QF>), dev::kBlock, lds));
     constexpr uint32_t kWavesPerBlock = dev::kBlock / 64;
     uint64_t resident = static_cast<uint64_t>(std::max(1, cus)) * std::max(1, per_cu);
     if (const char* e = std::getenv("CRT_GRID_BLOCKS"))  // schedule tests: a smaller grid, same frame
@@ -2200,11 +2250,11 @@ static int launch_render(const crt_scene* s, int device, const crt_camera* cam, 
             W.segments = knob("CRT_XCD_QUEUES", LSCENE ? 0 : 1) ? 8u : 1u;
             HIP_TRY(hipMemsetAsync(queue, 0, 8 * sizeof(uint32_t), stream));
             if (count) {
-                hipLaunchKernelGGL((dev::render_kernel<SE, GSTACK, LSCENE, true>), dim3(static_cast<uint32_t>(blocks)),
+                hipLaunchKernelGGL((dev::render_kernel<SE, GSTACK, LSCENE, true, QF>), dim3(static_cast<uint32_t>(blocks)),
                                    dim3(dev::kBlock), lds, stream, S, C, W, partial, gstack, ctr);
                 HIP_TRY(hipGetLastError());
             } else {
-                hipLaunchKernelGGL((dev::render_kernel<SE, GSTACK, LSCENE, false>), dim3(static_cast<uint32_t>(blocks)),
+                hipLaunchKernelGGL((dev::render_kernel<SE, GSTACK, LSCENE, false, QF>), dim3(static_cast<uint32_t>(blocks)),
                                    dim3(dev::kBlock), lds, stream, S, C, W, partial, gstack, ctr);
                 HIP_TRY(hipGetLastError());
                 const uint64_t rb = (static_cast<uint64_t>(W.bw) * W.bh + 255) / 256;
@@ -2273,7 +2323,8 @@ static int dispatch_render(const crt_scene* s, int device, const crt_camera* cam
     W.bytes_spheres = static_cast<uint32_t>(align16(s->spheres.size() * (W.spheres_f32 ? sizeof(DevSpherePair)
                                                                                          : sizeof(DevSphere))));
     W.bytes_quads = static_cast<uint32_t>(align16(s->quads.size() * sizeof(DevQuad)));
-    W.bytes_quadf = W.quads_f32 ? static_cast<uint32_t>(s->quads.size() * sizeof(DevQuadF)) : 0u;
+    W.bytes_quadf = W.quads_f32 ? static_cast<uint32_t>(s->quads.size() * (W.quads_flat ? sizeof(DevQuadBox) : sizeof(DevQuadF)))
+                                : 0u;
     const size_t scene_bytes = static_cast<size_t>(W.bytes_nodes) + W.bytes_refs + W.bytes_spheres + W.bytes_quads +
                                W.bytes_quadf;
     const uint32_t level = static_cast<uint32_t>(dev::kBlock * sizeof(SE));  // one stack level
@@ -2296,7 +2347,9 @@ static int dispatch_render(const crt_scene* s, int device, const crt_camera* cam
         if (W.spheres_f32 && kSph64Lds && stack_at(scene_bytes + sph64) + stack_bytes + align16(sizeof(dev::CamView)) <= kLdsSceneBudget)
             W.bytes_sph64 = sph64;
         W.lds_stack = stack_at(scene_bytes + W.bytes_sph64);
-        return launch_render<SE, false, true>(s, device, cam, W, W.lds_stack + stack_bytes, d_rgb, st, count_stats);
+        if (W.sphere_only)
+            return launch_render<SE, false, true, false>(s, device, cam, W, W.lds_stack + stack_bytes, d_rgb, st, count_stats);
+        return launch_render<SE, false, true, true>(s, device, cam, W, W.lds_stack + stack_bytes, d_rgb, st, count_stats);
     }
     // HBM scene: the top of the (breadth-first) node array goes to LDS as far as it fits beside
     // the stack without costing resident blocks (CRT_WAVES_PER_EU blocks of 4 waves, the VGPR
@@ -2312,11 +2365,11 @@ static int dispatch_render(const crt_scene* s, int device, const crt_camera* cam
         W.ntop = top_bytes(room);
         W.lds_nodes = 0;
         W.lds_stack = stack_at(align16(W.ntop));
-        return launch_render<SE, false, false>(s, device, cam, W, W.lds_stack + stack_bytes, d_rgb, st, count_stats);
+        return launch_render<SE, false, false, false>(s, device, cam, W, W.lds_stack + stack_bytes, d_rgb, st, count_stats);
     }
     W.ntop = top_bytes(per_block);
     W.lds_nodes = 0;
-    return launch_render<SE, true, false>(s, device, cam, W, W.ntop, d_rgb, st, count_stats);
+    return launch_render<SE, true, false, false>(s, device, cam, W, W.ntop, d_rgb, st, count_stats);
 }
 
 int device_render(const crt_scene* s, int device, const crt_camera* cam, const crt_tiling* t,
@@ -2358,6 +2411,8 @@ int device_render(const crt_scene* s, int device, const crt_camera* cam, const c
     W.sphere_only = (s->quads.empty() && !s->spheres.empty()) ? 1u : 0u;
     W.spheres_f32 = (W.sphere_only && s->dev[device].spheres_f32_ok) ? 1u : 0u;
     W.quads_f32 = (s->spheres.empty() && !s->quads.empty() && s->dev[device].quads_f32_ok) ? 1u : 0u;
+    // the flat-box filter is the walk's f32 node test: it needs the walk's f32 range (f32_ok)
+    W.quads_flat = (W.quads_f32 && s->dev[device].quads_flat_ok && s->dev[device].f32_ok) ? 1u : 0u;
     W.exact_slab = (s->exact_slab || std::getenv("CRT_EXACT_SLAB") != nullptr) ? 1u : 0u;
     hipStream_t st = static_cast<hipStream_t>(stream);
     if (count_stats) HIP_TRY(hipStreamCreate(&st));

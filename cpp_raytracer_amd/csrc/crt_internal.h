@@ -105,6 +105,8 @@ struct DeviceCopy {
     DevQuad* quads = nullptr;
     DevQuadF* quadf = nullptr;       // f32 filter records (crt_quad_filter.h)
     bool quads_f32_ok = false;       // every parallelogram within the filter's range
+    DevQuadBox* quadbox = nullptr;   // flat boxes of axis-aligned parallelograms (crt_quad_filter.h)
+    bool quads_flat_ok = false;      // every parallelogram axis-aligned: the flat-box filter applies
     uint32_t* quad_mat = nullptr;
     DevMaterial* mats = nullptr;
     // the material of every sphere / parallelogram slot (the render kernel's shading reads one

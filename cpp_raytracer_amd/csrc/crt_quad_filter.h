@@ -154,4 +154,59 @@ CRT_HD bool quad_candidate(const DevQuadF& q, const QuadRay32& L, Rcp rcp) {
     return !(den_ok & (t_out | a_out | b_out));
 }
 
+// ---- axis-aligned parallelograms: the walk's node test on a flat box ---------------------------
+// A parallelogram whose sides lie along two different axes i, j (every face of a Box, box.h:53-84,
+// and the Cornell walls) is the rectangle p_k = v_k, p_i in [a_i, b_i], p_j in [a_j, b_j]: the
+// flat box with a_k = b_k = v_k. Its unit normal and sn are exactly zero off axis k (each cross-
+// product component has a zero factor in both products), so the reference computes
+//   t = n_k (v_k - o_k) / (n_k d_k),   alpha = (p_i - v_i) / s1_i,   beta = (p_j - v_j) / s2_j
+// up to a few f64 roundings: within ~10 u64 (|t| + |o_i / d_i| + |v_i / d_i|) of the exact values
+// in t units (u64 = 2^-53; an alpha error e is a t error e |s1_i / d_i|). "alpha in [0, 1]" is
+// "t within the i-slab of the box", so the reference's hit is the slab test of the flat box
+// (t in (t_min, t_max), every slab containing t) up to those errors.
+// The filter runs the render kernel's f32 node test (crt_device.hip walk(): t'_jk = fma(b32_jk,
+// inv32_k, -oinv32_k), lo' = max of the mins and tmin', hi' = min of the maxes and tmax',
+// gap' = hi' - lo', th = 2^-19 max(|lo'|, |hi'|) + marg) on the box rounded to f32 and rejects
+// when gap' < -th. The walk's analysis bounds |gap' - gap64| by 2^-20.1 M + 2^-19.8 A + 2^-84
+// (M = max(|lo'|, |hi'|), A = max_k |o_k / d_k|, gap64 the f64 slab gap), so a rejection means
+// gap64 < -2^-20.3 (M + A): the ray misses the closed rectangle (or the (t_min, t_max) range) by
+// at least that much in exact arithmetic, ~2^30 times the reference's rounding errors above (|t|,
+// the bounding slab values and |v_i / d_i| <= |slab value| + A are all <= M + A where they
+// decide), so the reference misses it too, for this t_max and any smaller one. Rays outside the
+// walk's range carry marg = inf (every quad a candidate), and NaN never rejects.
+// tools/fuzz_quad_filter.cpp runs this sequence against the exact test.
+struct alignas(16) DevQuadBox {
+    float b[6];      // x.min x.max y.min y.max z.min z.max (RN32 of the f64 bounds)
+    uint32_t pad[2];
+};
+static_assert(sizeof(DevQuadBox) == 32, "flat quad box record");
+
+// the flat box of an axis-aligned parallelogram; false for any other one (or bounds beyond the
+// walk's 2^40 range)
+inline bool quad_flat_box(const double v[3], const double s1[3], const double s2[3], DevQuadBox& f) {
+    int a1 = -1, a2 = -1;
+    for (int k = 0; k < 3; ++k) {
+        if (s1[k] != 0) {
+            if (a1 >= 0) return false;
+            a1 = k;
+        }
+        if (s2[k] != 0) {
+            if (a2 >= 0) return false;
+            a2 = k;
+        }
+    }
+    if (a1 < 0 || a2 < 0 || a1 == a2) return false;
+    for (int k = 0; k < 3; ++k) {
+        double lo = v[k], hi = v[k];
+        const double e = k == a1 ? v[k] + s1[k] : k == a2 ? v[k] + s2[k] : v[k];
+        lo = std::fmin(lo, e);
+        hi = std::fmax(hi, e);
+        if (!(std::fabs(lo) <= 0x1p40 && std::fabs(hi) <= 0x1p40)) return false;
+        f.b[2 * k] = static_cast<float>(lo);
+        f.b[2 * k + 1] = static_cast<float>(hi);
+    }
+    f.pad[0] = f.pad[1] = 0;
+    return true;
+}
+
 }  // namespace crt

@@ -236,3 +236,46 @@ def test_tall_and_wide_frames(crt, w, h, crops):
     assert np.isfinite(out).all()
     for r0, r1, c0, c1 in crops:
         check(out[r0:r1, c0:c1], orc.render(d, 45, threads=8, crop=(r0, r1, c0, c1)))
+
+
+def _box_room(crt, seed, n_boxes, **cam):
+    """The Cornell room plus random axis-aligned boxes and wall-flush light panels on a coarse
+    grid: coincident faces, boxes touching the walls and each other, rays grazing shared planes."""
+    from cpp_raytracer_amd import OBJECT_DTYPE
+    d = scene(crt, "cornell", **cam)
+    rng = np.random.default_rng(seed)
+    objs = [o for o in d.objects]
+    for _ in range(n_boxes):
+        a = rng.integers(0, 15, 3) * 37.0
+        b = a + rng.integers(1, 5, 3) * 37.0
+        o = np.zeros(1, OBJECT_DTYPE)[0]
+        o["kind"], o["material"] = 3, rng.integers(0, len(d.materials))  # CRT_BOX
+        o["v"][:6] = np.concatenate([a, np.minimum(b, 555.0)])
+        objs.append(o)
+    for _ in range(3):  # light panels lying on a wall plane
+        o = np.zeros(1, OBJECT_DTYPE)[0]
+        o["kind"], o["material"] = 2, int(np.flatnonzero(d.materials["kind"] == 4)[0])  # CRT_PARALLELOGRAM, the light
+        ax = rng.integers(0, 3)
+        v = rng.integers(1, 12, 3) * 37.0
+        v[ax] = 555.0 * rng.integers(0, 2)
+        s1, s2 = np.zeros(3), np.zeros(3)
+        s1[(ax + 1) % 3], s2[(ax + 2) % 3] = 74.0, -74.0
+        o["v"][:] = np.concatenate([v, s1, s2])
+        objs.append(o)
+    d.objects = np.array(objs, dtype=OBJECT_DTYPE)
+    return d
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_flat_box_quad_filter(crt, monkeypatch, seed):
+    """Axis-aligned parallelograms take the flat-box filter (the walk's f32 node test on each
+    one's box, crt_quad_filter.h): frames equal the oracle's, and are bit-identical to the generic
+    f32 filter (CRT_GENERIC_QUADS) and to every parallelogram decided in f64 (CRT_F64_QUADS)."""
+    d = _box_room(crt, seed, 12, image_w=72, image_h=72, samples_per_pixel=6, max_depth=60)
+    flat = gpu(crt, d, 50 + seed)
+    check(flat, orc.render(d, 50 + seed, threads=8))
+    monkeypatch.setenv("CRT_GENERIC_QUADS", "1")
+    assert np.array_equal(flat, gpu(crt, d, 50 + seed))
+    monkeypatch.delenv("CRT_GENERIC_QUADS")
+    monkeypatch.setenv("CRT_F64_QUADS", "1")
+    assert np.array_equal(flat, gpu(crt, d, 50 + seed))

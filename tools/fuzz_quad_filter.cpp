@@ -91,6 +91,31 @@ static void rand_dir(double s, double d[3]) {
 }
 
 static long viol = 0, miss_total = 0, miss_rejected = 0, hits = 0, skipped = 0;
+static long fviol = 0, fmiss_total = 0, fmiss_rejected = 0, fhits = 0;
+
+// the render kernel's flat-box filter for axis-aligned parallelograms (crt_device.hip leaf_step):
+// the walk's f32 node test, with the ray constants of trav_init (inv32 = v_rcp_f32(RN32(d)),
+// oinv32 = RN32(RN32(o) inv32), marg) and tmin' = RN32(t_min), tmax' = RN32(min(t_max, 2^100))
+static bool flat_candidate(const crt::DevQuadBox& b, const double o[3], const double d[3], double tmin,
+                           double tmax) {
+    float inv[3], oinv[3], A = 0;
+    bool f32 = true;
+    for (int k = 0; k < 3; ++k) {
+        const float d32 = static_cast<float>(d[k]), o32 = static_cast<float>(o[k]);
+        inv[k] = rcp_adversarial(d32);
+        oinv[k] = o32 * inv[k];
+        A = std::fmax(A, std::fabs(oinv[k]));
+        f32 = f32 && std::fabs(d32) <= 0x1p39f && std::fabs(d32) >= 0x1p-39f && std::fabs(o32) <= 0x1p40f;
+    }
+    const float marg = f32 ? std::fmax(A * 0x1p-19f, 0x1p-60f) : INFINITY;
+    const float tmin32 = static_cast<float>(tmin), tmax32 = static_cast<float>(std::fmin(tmax, 0x1p100));
+    float t[6];
+    for (int j = 0; j < 6; ++j) t[j] = std::fma(b.b[j], inv[j / 2], -oinv[j / 2]);
+    const float lo = std::fmax(std::fmax(std::fmin(t[0], t[1]), std::fmin(t[2], t[3])), std::fmax(std::fmin(t[4], t[5]), tmin32));
+    const float hi = std::fmin(std::fmin(std::fmax(t[0], t[1]), std::fmax(t[2], t[3])), std::fmin(std::fmax(t[4], t[5]), tmax32));
+    const float th = std::fma(std::fmax(std::fabs(lo), std::fabs(hi)), 0x1p-19f, marg);
+    return !(hi - lo < -th);
+}
 
 static void check(const Quad& q, const double o[3], const double d[3], double tmin, double tmax) {
     DevQuadF f;
@@ -99,6 +124,20 @@ static void check(const Quad& q, const double o[3], const double d[3], double tm
     crt::quad_ray32(o, d, tmin, tmax, L);
     const bool cand = crt::quad_candidate(f, L, rcp_adversarial);
     const bool hit = exact(q, o, d, tmin, tmax, nullptr);
+    crt::DevQuadBox box;
+    if (crt::quad_flat_box(q.v, q.s1, q.s2, box)) {
+        const bool fc = flat_candidate(box, o, d, tmin, tmax);
+        if (hit) {
+            ++fhits;
+            if (!fc && ++fviol <= 10)
+                std::printf("FLAT VIOLATION o=(%a %a %a) d=(%a %a %a) v=(%a %a %a) s1=(%a %a %a) s2=(%a %a %a) tmin=%a tmax=%a\n",
+                            o[0], o[1], o[2], d[0], d[1], d[2], q.v[0], q.v[1], q.v[2], q.s1[0], q.s1[1], q.s1[2],
+                            q.s2[0], q.s2[1], q.s2[2], tmin, tmax);
+        } else {
+            ++fmiss_total;
+            fmiss_rejected += !fc;
+        }
+    }
     if (hit) {
         ++hits;
         if (!cand) {
@@ -118,7 +157,7 @@ static Quad rand_quad(double S) {
     for (int k = 0; k < 3; ++k) v[k] = urange(-S, S);
     rand_dir(S * urange(0.05, 1), s1);
     rand_dir(S * urange(0.05, 1), s2);
-    if (u01() < 0.3) {  // axis-aligned (Cornell walls and boxes)
+    if (u01() < 0.5) {  // axis-aligned (Cornell walls and boxes)
         const int a = static_cast<int>(next_u64() % 3), b = (a + 1 + static_cast<int>(next_u64() % 2)) % 3;
         for (int k = 0; k < 3; ++k) { s1[k] = 0; s2[k] = 0; }
         s1[a] = S * urange(0.05, 1) * (u01() < 0.5 ? -1 : 1);
@@ -194,5 +233,8 @@ int main(int argc, char** argv) {
     std::printf("cases %ld (skipped %ld): exact hits %ld, violations %ld; exact misses %ld, rejected by the "
                 "filter %.4f\n", 5 * M, skipped, hits, viol, miss_total,
                 miss_total ? static_cast<double>(miss_rejected) / miss_total : 0.0);
-    return viol != 0;
+    std::printf("flat-box filter (axis-aligned parallelograms): exact hits %ld, violations %ld; exact misses %ld, "
+                "rejected %.4f\n", fhits, fviol, fmiss_total,
+                fmiss_total ? static_cast<double>(fmiss_rejected) / fmiss_total : 0.0);
+    return viol != 0 || fviol != 0;
 }

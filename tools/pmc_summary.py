@@ -20,7 +20,7 @@ from pathlib import Path
 sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 from bench import kernel_source_sha  # noqa: E402
 
-KERNEL = "crt::dev::render_kernel<unsigned short, false, true, false>"
+KERNEL = "crt::dev::render_kernel<unsigned short, false, true, false, false>"  # sphere-only LDS scene, timed pass
 
 
 def main():
