@@ -581,7 +581,7 @@ __device__ __forceinline__ DevSphere sphere_at(const SceneView& S, uint32_t i) {
 // Resolve the hit record (hittable.h:46-71): hit point ray(t), outward normal, front face.
 // IR: the sphere's 1/r comes in as ir (shade: the slot's material record holds RN(1/r), the
 // same value the division gives); otherwise it is divided here.
-template <bool LS, bool IR = false>
+template <bool LS, bool IR = false, bool SPH = false>
 __device__ __forceinline__ uint32_t hit_record(const SceneView& S, uint32_t ref, const double o[3],
                                                const double d[3], double t, double p[3],
                                                double nrm[3], bool& front, double ir_in = 0) {
@@ -590,7 +590,7 @@ __device__ __forceinline__ uint32_t hit_record(const SceneView& S, uint32_t ref,
     p[2] = o[2] + d[2] * t;
     double nx, ny, nz;
     uint32_t m;
-    if (ref & kRefQuad) {
+    if (!SPH && (ref & kRefQuad)) {
         if constexpr (LS) {
             const DevQuad q = lds_rec<DevQuad>(S.quads_lds + ((ref & ~kRefQuad) << 7));
             nx = q.n[0]; ny = q.n[1]; nz = q.n[2];
@@ -1348,7 +1348,7 @@ __device__ __forceinline__ void start_path(const CamView& C, uint32_t row, uint3
 // One level of ray_color (camera.h:205-258) after the closest-hit query: scatters
 // (material.h:64-263) into the next ray, or ends the path adding T * (background | emission) to
 // acc. Returns true when the path has ended (miss, light, absorption).
-template <bool LS>
+template <bool LS, bool SPH = false>
 __device__ __forceinline__ bool shade(const SceneView& S, const CamView& C, Path& P, bool hit,
                                       uint32_t ref, double t, double acc[3]) {
     if (!hit) {
@@ -1358,10 +1358,10 @@ __device__ __forceinline__ bool shade(const SceneView& S, const CamView& C, Path
         return true;
     }
     // the slot's material record, loaded first (its address needs only the slot)
-    const DevMaterial& M = (ref & kRefQuad) ? S.quad_mrec[ref & ~kRefQuad] : S.sphere_mrec[ref];
+    const DevMaterial& M = (!SPH && (ref & kRefQuad)) ? S.quad_mrec[ref & ~kRefQuad] : S.sphere_mrec[ref];
     double p[3], n[3];
     bool front;
-    (void)hit_record<LS, true>(S, ref, P.o, P.d, t, p, n, front, M.emit[0]);
+    (void)hit_record<LS, true, SPH>(S, ref, P.o, P.d, t, p, n, front, M.emit[0]);
     const uint32_t kind = M.kind;
     const bool lam = kind == CRT_LAMBERTIAN, met = kind == CRT_METAL, die = kind == CRT_DIELECTRIC;
     if (!(lam || met || die)) {  // DiffuseLight: emits, never scatters (material.h:248-263)
@@ -1534,6 +1534,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LSCENE ?
     SceneView Sg, CamView C, Work W, double* __restrict__ partial, SE* __restrict__ gstack,
     Counters* __restrict__ counters) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    // the LDS-scene instance without the quad filters is launched for sphere-only scenes only:
+    // the parallelogram paths of the leaf and shading code are compiled out of it
+    constexpr bool kSphOnly = LSCENE && !QF;
     SceneView S = Sg;
     if (LSCENE) {  // f32 nodes at LDS offset 0 (fetch_nodef: a node's LDS address is its ref)
         if (static_cast<uint32_t>(reinterpret_cast<uintptr_t>((LdsByte*)smem)) != 0) __builtin_trap();
@@ -1719,7 +1722,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LSCENE ?
                 if (wave_leader()) atomicAdd(&counters->round_leaves, nl);
             }
             if (COUNT) cl -= static_cast<uint32_t>(wall_clock64());
-            if (R.state == kLeaf) leaf_step<SE, COUNT, kTopTreelet && !LSCENE, LSCENE>(S, st, P.o, P.d, C.t_min, tmin32, W.sphere_only != 0, W.spheres_f32 != 0, QF && W.quads_f32 != 0, QF && W.quads_flat != 0, R, ctr);
+            if (R.state == kLeaf) leaf_step<SE, COUNT, kTopTreelet && !LSCENE, LSCENE>(S, st, P.o, P.d, C.t_min, tmin32, kSphOnly || W.sphere_only != 0, W.spheres_f32 != 0, QF && W.quads_f32 != 0, QF && W.quads_flat != 0, R, ctr);
             if (COUNT) cl += static_cast<uint32_t>(wall_clock64());
             const uint64_t pending = __ballot(R.state == kWalk);
             const uint64_t finished = __ballot(R.state == kDone);
@@ -1738,7 +1741,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LSCENE ?
             flush_counts(ctr, counters);
         if (R.state == kDone) {
             if (COUNT && wave_leader()) ctr.it_shade++;
-            bool ended = shade<LSCENE>(S, CL, P, R.found, R.ref, R.tmax, acc);
+            bool ended = shade<LSCENE, kSphOnly>(S, CL, P, R.found, R.ref, R.tmax, acc);
             // a scattered ray with no bounce left returns RGB::zero() (camera.h:211-213)
             if (!ended && P.depth == 0) ended = true;
             if (!ended) {
