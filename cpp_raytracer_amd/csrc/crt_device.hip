@@ -1527,16 +1527,16 @@ __device__ __forceinline__ void set_prio() {
 #endif
 constexpr bool kRoundCounters = CRT_ROUND_COUNTERS != 0;
 
-// QF: the instance has the parallelogram filters' leaf passes (sphere-only scenes launch the
-// instance without them: their code is not in the kernel at all)
+// QF: the instance handles parallelograms (their filters' leaf passes, their hit records);
+// sphere-only scenes launch the instance without them
 template <typename SE, bool GSTACK, bool LSCENE, bool COUNT, bool QF>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LSCENE ? CRT_WAVES_PER_EU_LDS : CRT_WAVES_PER_EU, 8))) void render_kernel(
     SceneView Sg, CamView C, Work W, double* __restrict__ partial, SE* __restrict__ gstack,
     Counters* __restrict__ counters) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    // the LDS-scene instance without the quad filters is launched for sphere-only scenes only:
-    // the parallelogram paths of the leaf and shading code are compiled out of it
-    constexpr bool kSphOnly = LSCENE && !QF;
+    // the instances with QF = false are launched for sphere-only scenes only: the parallelogram
+    // paths of the leaf and shading code are compiled out of them
+    constexpr bool kSphOnly = !QF;
     SceneView S = Sg;
     if (LSCENE) {  // f32 nodes at LDS offset 0 (fetch_nodef: a node's LDS address is its ref)
         if (static_cast<uint32_t>(reinterpret_cast<uintptr_t>((LdsByte*)smem)) != 0) __builtin_trap();
@@ -2368,11 +2368,14 @@ static int dispatch_render(const crt_scene* s, int device, const crt_camera* cam
         W.ntop = top_bytes(room);
         W.lds_nodes = 0;
         W.lds_stack = stack_at(align16(W.ntop));
-        return launch_render<SE, false, false, false>(s, device, cam, W, W.lds_stack + stack_bytes, d_rgb, st, count_stats);
+        if (W.sphere_only)
+            return launch_render<SE, false, false, false>(s, device, cam, W, W.lds_stack + stack_bytes, d_rgb, st, count_stats);
+        return launch_render<SE, false, false, true>(s, device, cam, W, W.lds_stack + stack_bytes, d_rgb, st, count_stats);
     }
     W.ntop = top_bytes(per_block);
     W.lds_nodes = 0;
-    return launch_render<SE, true, false, false>(s, device, cam, W, W.ntop, d_rgb, st, count_stats);
+    if (W.sphere_only) return launch_render<SE, true, false, false>(s, device, cam, W, W.ntop, d_rgb, st, count_stats);
+    return launch_render<SE, true, false, true>(s, device, cam, W, W.ntop, d_rgb, st, count_stats);
 }
 
 int device_render(const crt_scene* s, int device, const crt_camera* cam, const crt_tiling* t,

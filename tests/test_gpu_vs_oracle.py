@@ -279,3 +279,20 @@ def test_flat_box_quad_filter(crt, monkeypatch, seed):
     monkeypatch.delenv("CRT_GENERIC_QUADS")
     monkeypatch.setenv("CRT_F64_QUADS", "1")
     assert np.array_equal(flat, gpu(crt, d, 50 + seed))
+
+
+@pytest.mark.parametrize("name,kw", [
+    ("cornell", dict(image_w=48, image_h=48, samples_per_pixel=4, max_depth=100)),
+    ("rtow_final_lights", dict(image_w=80, image_h=45, samples_per_pixel=4)),
+    ("parallelograms", dict(image_w=48, image_h=48, samples_per_pixel=4)),
+])
+@pytest.mark.parametrize("gstack", [False, True])
+def test_hbm_scene_kernels_with_parallelograms(crt, monkeypatch, name, kw, gstack):
+    """The HBM-scene kernels (scene in HBM: CRT_NO_LDS_SCENE; stack in LDS or, CRT_FORCE_GSTACK,
+    in HBM) on scenes with parallelograms, which launch the instances with the parallelogram
+    paths (QF): frames equal the oracle's."""
+    monkeypatch.setenv("CRT_NO_LDS_SCENE", "1")
+    if gstack:
+        monkeypatch.setenv("CRT_FORCE_GSTACK", "1")
+    d = scene(crt, name, **kw)
+    check(gpu(crt, d, 60), orc.render(d, 60, threads=8))
