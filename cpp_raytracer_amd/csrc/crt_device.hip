@@ -1529,8 +1529,10 @@ constexpr bool kRoundCounters = CRT_ROUND_COUNTERS != 0;
 
 // QF: the instance handles parallelograms (their filters' leaf passes, their hit records);
 // sphere-only scenes launch the instance without them
-template <typename SE, bool GSTACK, bool LSCENE, bool COUNT, bool QF>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LSCENE ? CRT_WAVES_PER_EU_LDS : CRT_WAVES_PER_EU, 8))) void render_kernel(
+// W5: 5 waves per SIMD (96 VGPRs, ~48 of them spilled), launched for sphere-only LDS scenes whose
+// LDS copy leaves room for five blocks per CU (dispatch_render)
+template <typename SE, bool GSTACK, bool LSCENE, bool COUNT, bool QF, bool W5>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W5 ? 5 : LSCENE ? CRT_WAVES_PER_EU_LDS : CRT_WAVES_PER_EU, 8))) void render_kernel(
     SceneView Sg, CamView C, Work W, double* __restrict__ partial, SE* __restrict__ gstack,
     Counters* __restrict__ counters) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -2119,6 +2121,10 @@ static uint32_t count_owned(uint32_t h, uint32_t rb, uint32_t tc, uint32_t ti) {
 
 static size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
 
+#ifndef CRT_FIVE_WAVES
+#define CRT_FIVE_WAVES 1
+#endif
+constexpr bool kFiveWaves = CRT_FIVE_WAVES != 0;  // the 5-wave instance for small sphere-only LDS scenes
 #ifndef CRT_LDS_BUDGET_KB
 #define CRT_LDS_BUDGET_KB 40
 #endif
@@ -2141,7 +2147,7 @@ static size_t partial_budget() {
     return size_t{4} << 30;
 }
 
-template <typename SE, bool GSTACK, bool LSCENE, bool QF>
+template <typename SE, bool GSTACK, bool LSCENE, bool QF, bool W5 = false>
 static int launch_render(const crt_scene* s, int device, const crt_camera* cam, const dev::Work& w0,
                          size_t lds, double* d_rgb, hipStream_t stream, crt_render_stats* count_stats) {
     const DeviceCopy& c = s->dev[device];
@@ -2179,7 +2185,7 @@ static int launch_render(const crt_scene* s, int device, const crt_camera* cam, 
     int cus = 0, per_cu = 0;
     HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
     HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &per_cu, reinterpret_cast<const void*>(dev::render_kernel<SE, GSTACK, LSCENE, false, QF>), dev::kBlock, lds));
+        &per_cu, reinterpret_cast<const void*>(dev::render_kernel<SE, GSTACK, LSCENE, false, QF, W5>), dev::kBlock, lds));
     constexpr uint32_t kWavesPerBlock = dev::kBlock / 64;
     uint64_t resident = static_cast<uint64_t>(std::max(1, cus)) * std::max(1, per_cu);
     if (const char* e = std::getenv("CRT_GRID_BLOCKS"))  // schedule tests: a smaller grid, same frame
@@ -2253,11 +2259,11 @@ static int launch_render(const crt_scene* s, int device, const crt_camera* cam, 
             W.segments = knob("CRT_XCD_QUEUES", LSCENE ? 0 : 1) ? 8u : 1u;
             HIP_TRY(hipMemsetAsync(queue, 0, 8 * sizeof(uint32_t), stream));
             if (count) {
-                hipLaunchKernelGGL((dev::render_kernel<SE, GSTACK, LSCENE, true, QF>), dim3(static_cast<uint32_t>(blocks)),
+                hipLaunchKernelGGL((dev::render_kernel<SE, GSTACK, LSCENE, true, QF, W5>), dim3(static_cast<uint32_t>(blocks)),
                                    dim3(dev::kBlock), lds, stream, S, C, W, partial, gstack, ctr);
                 HIP_TRY(hipGetLastError());
             } else {
-                hipLaunchKernelGGL((dev::render_kernel<SE, GSTACK, LSCENE, false, QF>), dim3(static_cast<uint32_t>(blocks)),
+                hipLaunchKernelGGL((dev::render_kernel<SE, GSTACK, LSCENE, false, QF, W5>), dim3(static_cast<uint32_t>(blocks)),
                                    dim3(dev::kBlock), lds, stream, S, C, W, partial, gstack, ctr);
                 HIP_TRY(hipGetLastError());
                 const uint64_t rb = (static_cast<uint64_t>(W.bw) * W.bh + 255) / 256;
@@ -2346,10 +2352,21 @@ static int dispatch_render(const crt_scene* s, int device, const crt_camera* cam
         W.lds_quads = W.lds_spheres + W.bytes_spheres;
         W.lds_quadf = W.lds_quads + W.bytes_quads;
         W.lds_sph64 = W.lds_quadf + W.bytes_quadf;
+        const size_t cam_bytes = align16(sizeof(dev::CamView));
+        // Sphere-only scenes run five waves per SIMD when five blocks fit a CU's LDS (32 KB each),
+        // staging the f64 spheres only if they fit that too (config 2: 73.7 ms at five waves
+        // without them vs 75.8 at four with them); the others four, with up to 40 KB. Parallelogram
+        // scenes keep four (config 3 at five: 116.5 vs 100.6 ms).
+        const size_t budget5 = 160 * 1024 / 5;
+        const bool w5 = W.sphere_only && kFiveWaves && std::getenv("CRT_FOUR_WAVES") == nullptr &&
+                        stack_at(scene_bytes) + stack_bytes + cam_bytes <= budget5;
+        const size_t budget = w5 ? budget5 : kLdsSceneBudget;
         const uint32_t sph64 = static_cast<uint32_t>(s->spheres.size() * sizeof(DevSphere));
-        if (W.spheres_f32 && kSph64Lds && stack_at(scene_bytes + sph64) + stack_bytes + align16(sizeof(dev::CamView)) <= kLdsSceneBudget)
+        if (W.spheres_f32 && kSph64Lds && stack_at(scene_bytes + sph64) + stack_bytes + cam_bytes <= budget)
             W.bytes_sph64 = sph64;
         W.lds_stack = stack_at(scene_bytes + W.bytes_sph64);
+        if (w5)
+            return launch_render<SE, false, true, false, true>(s, device, cam, W, W.lds_stack + stack_bytes, d_rgb, st, count_stats);
         if (W.sphere_only)
             return launch_render<SE, false, true, false>(s, device, cam, W, W.lds_stack + stack_bytes, d_rgb, st, count_stats);
         return launch_render<SE, false, true, true>(s, device, cam, W, W.lds_stack + stack_bytes, d_rgb, st, count_stats);

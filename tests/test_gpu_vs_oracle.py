@@ -296,3 +296,14 @@ def test_hbm_scene_kernels_with_parallelograms(crt, monkeypatch, name, kw, gstac
         monkeypatch.setenv("CRT_FORCE_GSTACK", "1")
     d = scene(crt, name, **kw)
     check(gpu(crt, d, 60), orc.render(d, 60, threads=8))
+
+
+def test_five_wave_instance_equals_four_wave(crt, monkeypatch):
+    """Small sphere-only LDS scenes run the 5-wave instance (96 VGPRs, spills, no f64 spheres in
+    LDS); the 4-wave instance (CRT_FOUR_WAVES) gives the same frame bit for bit, and both the
+    oracle's."""
+    d = scene(crt, "rtow_final", 42, image_w=96, image_h=64, samples_per_pixel=8, max_depth=50)
+    five = gpu(crt, d, 70)
+    check(five, orc.render(d, 70, threads=8))
+    monkeypatch.setenv("CRT_FOUR_WAVES", "1")
+    assert np.array_equal(five, gpu(crt, d, 70))
