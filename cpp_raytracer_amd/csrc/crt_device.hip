@@ -581,7 +581,7 @@ __device__ __forceinline__ DevSphere sphere_at(const SceneView& S, uint32_t i) {
 // Resolve the hit record (hittable.h:46-71): hit point ray(t), outward normal, front face.
 // IR: the sphere's 1/r comes in as ir (shade: the slot's material record holds RN(1/r), the
 // same value the division gives); otherwise it is divided here.
-template <bool LS, bool IR = false, bool SPH = false>
+template <bool LS, bool IR = false, bool SPH = false, bool QONLY = false>
 __device__ __forceinline__ uint32_t hit_record(const SceneView& S, uint32_t ref, const double o[3],
                                                const double d[3], double t, double p[3],
                                                double nrm[3], bool& front, double ir_in = 0) {
@@ -590,7 +590,7 @@ __device__ __forceinline__ uint32_t hit_record(const SceneView& S, uint32_t ref,
     p[2] = o[2] + d[2] * t;
     double nx, ny, nz;
     uint32_t m;
-    if (!SPH && (ref & kRefQuad)) {
+    if (QONLY || (!SPH && (ref & kRefQuad))) {
         if constexpr (LS) {
             const DevQuad q = lds_rec<DevQuad>(S.quads_lds + ((ref & ~kRefQuad) << 7));
             nx = q.n[0]; ny = q.n[1]; nz = q.n[2];
@@ -1204,7 +1204,7 @@ __device__ __forceinline__ void leaf_step(const SceneView& S, Stack<SE>& st, con
                 R.found = true;
             }
         }
-    } else if (LS && qfilter && range.y <= 32 && quad_ray32_ok(o, d)) {
+    } else if (LS && qfilter && !qflat && range.y <= 32 && quad_ray32_ok(o, d)) {
         // parallelogram-only scenes (a slot is its parallelogram's index): the same two passes,
         // with the f32 filter of crt_quad_filter.h (quad_candidate) in pass 1. LDS-scene kernels
         // only: in the HBM-scene kernels its registers cost spills (none of the reference's
@@ -1348,7 +1348,7 @@ __device__ __forceinline__ void start_path(const CamView& C, uint32_t row, uint3
 // One level of ray_color (camera.h:205-258) after the closest-hit query: scatters
 // (material.h:64-263) into the next ray, or ends the path adding T * (background | emission) to
 // acc. Returns true when the path has ended (miss, light, absorption).
-template <bool LS, bool SPH = false>
+template <bool LS, bool SPH = false, bool QONLY = false>
 __device__ __forceinline__ bool shade(const SceneView& S, const CamView& C, Path& P, bool hit,
                                       uint32_t ref, double t, double acc[3]) {
     if (!hit) {
@@ -1358,10 +1358,10 @@ __device__ __forceinline__ bool shade(const SceneView& S, const CamView& C, Path
         return true;
     }
     // the slot's material record, loaded first (its address needs only the slot)
-    const DevMaterial& M = (!SPH && (ref & kRefQuad)) ? S.quad_mrec[ref & ~kRefQuad] : S.sphere_mrec[ref];
+    const DevMaterial& M = (QONLY || (!SPH && (ref & kRefQuad))) ? S.quad_mrec[ref & ~kRefQuad] : S.sphere_mrec[ref];
     double p[3], n[3];
     bool front;
-    (void)hit_record<LS, true, SPH>(S, ref, P.o, P.d, t, p, n, front, M.emit[0]);
+    (void)hit_record<LS, true, SPH, QONLY>(S, ref, P.o, P.d, t, p, n, front, M.emit[0]);
     const uint32_t kind = M.kind;
     const bool lam = kind == CRT_LAMBERTIAN, met = kind == CRT_METAL, die = kind == CRT_DIELECTRIC;
     if (!(lam || met || die)) {  // DiffuseLight: emits, never scatters (material.h:248-263)
@@ -1527,18 +1527,19 @@ __device__ __forceinline__ void set_prio() {
 #endif
 constexpr bool kRoundCounters = CRT_ROUND_COUNTERS != 0;
 
-// QF: the instance handles parallelograms (their filters' leaf passes, their hit records);
-// sphere-only scenes launch the instance without them
-// W5: 5 waves per SIMD (96 VGPRs, ~48 of them spilled), launched for sphere-only LDS scenes whose
-// LDS copy leaves room for five blocks per CU (dispatch_render)
-template <typename SE, bool GSTACK, bool LSCENE, bool COUNT, bool QF, bool W5>
+// PM (primitive mix): 0 sphere-only scenes (every parallelogram path compiled out), 1 any scene,
+// 2 parallelogram-only scenes of axis-aligned parallelograms (LDS scenes: the flat-box filter
+// only, no sphere paths)
+// W5: 5 waves per SIMD (96 VGPRs, ~40-48 of them spilled), launched for sphere-only and
+// flat-parallelogram LDS scenes whose LDS copy leaves room for five blocks per CU (dispatch_render)
+template <typename SE, bool GSTACK, bool LSCENE, bool COUNT, int PM, bool W5>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W5 ? 5 : LSCENE ? CRT_WAVES_PER_EU_LDS : CRT_WAVES_PER_EU, 8))) void render_kernel(
     SceneView Sg, CamView C, Work W, double* __restrict__ partial, SE* __restrict__ gstack,
     Counters* __restrict__ counters) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    // the instances with QF = false are launched for sphere-only scenes only: the parallelogram
-    // paths of the leaf and shading code are compiled out of them
-    constexpr bool kSphOnly = !QF;
+    // the instances with PM = 0 are launched for sphere-only scenes only, PM = 2 for scenes of
+    // axis-aligned parallelograms only: the other primitive's paths are compiled out of them
+    constexpr bool kSphOnly = PM == 0, kFlatOnly = PM == 2;
     SceneView S = Sg;
     if (LSCENE) {  // f32 nodes at LDS offset 0 (fetch_nodef: a node's LDS address is its ref)
         if (static_cast<uint32_t>(reinterpret_cast<uintptr_t>((LdsByte*)smem)) != 0) __builtin_trap();
@@ -1724,7 +1725,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W5 ? 5 :
                 if (wave_leader()) atomicAdd(&counters->round_leaves, nl);
             }
             if (COUNT) cl -= static_cast<uint32_t>(wall_clock64());
-            if (R.state == kLeaf) leaf_step<SE, COUNT, kTopTreelet && !LSCENE, LSCENE>(S, st, P.o, P.d, C.t_min, tmin32, kSphOnly || W.sphere_only != 0, W.spheres_f32 != 0, QF && W.quads_f32 != 0, QF && W.quads_flat != 0, R, ctr);
+            if (R.state == kLeaf) leaf_step<SE, COUNT, kTopTreelet && !LSCENE, LSCENE>(S, st, P.o, P.d, C.t_min, tmin32, kSphOnly || (!kFlatOnly && W.sphere_only != 0), !kFlatOnly && W.spheres_f32 != 0, kFlatOnly || (!kSphOnly && W.quads_f32 != 0), kFlatOnly || (!kSphOnly && W.quads_flat != 0), R, ctr);
             if (COUNT) cl += static_cast<uint32_t>(wall_clock64());
             const uint64_t pending = __ballot(R.state == kWalk);
             const uint64_t finished = __ballot(R.state == kDone);
@@ -1743,7 +1744,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W5 ? 5 :
             flush_counts(ctr, counters);
         if (R.state == kDone) {
             if (COUNT && wave_leader()) ctr.it_shade++;
-            bool ended = shade<LSCENE, kSphOnly>(S, CL, P, R.found, R.ref, R.tmax, acc);
+            bool ended = shade<LSCENE, kSphOnly, kFlatOnly>(S, CL, P, R.found, R.ref, R.tmax, acc);
             // a scattered ray with no bounce left returns RGB::zero() (camera.h:211-213)
             if (!ended && P.depth == 0) ended = true;
             if (!ended) {
@@ -2147,7 +2148,7 @@ static size_t partial_budget() {
     return size_t{4} << 30;
 }
 
-template <typename SE, bool GSTACK, bool LSCENE, bool QF, bool W5 = false>
+template <typename SE, bool GSTACK, bool LSCENE, int PM, bool W5 = false>
 static int launch_render(const crt_scene* s, int device, const crt_camera* cam, const dev::Work& w0,
                          size_t lds, double* d_rgb, hipStream_t stream, crt_render_stats* count_stats) {
     const DeviceCopy& c = s->dev[device];
@@ -2185,7 +2186,7 @@ static int launch_render(const crt_scene* s, int device, const crt_camera* cam, 
     int cus = 0, per_cu = 0;
     HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
     HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &per_cu, reinterpret_cast<const void*>(dev::render_kernel<SE, GSTACK, LSCENE, false, QF, W5>), dev::kBlock, lds));
+        &per_cu, reinterpret_cast<const void*>(dev::render_kernel<SE, GSTACK, LSCENE, false, PM, W5>), dev::kBlock, lds));
     constexpr uint32_t kWavesPerBlock = dev::kBlock / 64;
     uint64_t resident = static_cast<uint64_t>(std::max(1, cus)) * std::max(1, per_cu);
     if (const char* e = std::getenv("CRT_GRID_BLOCKS"))  // schedule tests: a smaller grid, same frame
@@ -2259,11 +2260,11 @@ static int launch_render(const crt_scene* s, int device, const crt_camera* cam, 
             W.segments = knob("CRT_XCD_QUEUES", LSCENE ? 0 : 1) ? 8u : 1u;
             HIP_TRY(hipMemsetAsync(queue, 0, 8 * sizeof(uint32_t), stream));
             if (count) {
-                hipLaunchKernelGGL((dev::render_kernel<SE, GSTACK, LSCENE, true, QF, W5>), dim3(static_cast<uint32_t>(blocks)),
+                hipLaunchKernelGGL((dev::render_kernel<SE, GSTACK, LSCENE, true, PM, W5>), dim3(static_cast<uint32_t>(blocks)),
                                    dim3(dev::kBlock), lds, stream, S, C, W, partial, gstack, ctr);
                 HIP_TRY(hipGetLastError());
             } else {
-                hipLaunchKernelGGL((dev::render_kernel<SE, GSTACK, LSCENE, false, QF, W5>), dim3(static_cast<uint32_t>(blocks)),
+                hipLaunchKernelGGL((dev::render_kernel<SE, GSTACK, LSCENE, false, PM, W5>), dim3(static_cast<uint32_t>(blocks)),
                                    dim3(dev::kBlock), lds, stream, S, C, W, partial, gstack, ctr);
                 HIP_TRY(hipGetLastError());
                 const uint64_t rb = (static_cast<uint64_t>(W.bw) * W.bh + 255) / 256;
@@ -2353,23 +2354,27 @@ static int dispatch_render(const crt_scene* s, int device, const crt_camera* cam
         W.lds_quadf = W.lds_quads + W.bytes_quads;
         W.lds_sph64 = W.lds_quadf + W.bytes_quadf;
         const size_t cam_bytes = align16(sizeof(dev::CamView));
-        // Sphere-only scenes run five waves per SIMD when five blocks fit a CU's LDS (32 KB each),
-        // staging the f64 spheres only if they fit that too (config 2: 73.7 ms at five waves
-        // without them vs 75.8 at four with them); the others four, with up to 40 KB. Parallelogram
-        // scenes keep four (config 3 at five: 116.5 vs 100.6 ms).
+        // Sphere-only scenes and scenes of axis-aligned parallelograms run five waves per SIMD when
+        // five blocks fit a CU's LDS (32 KB each), staging the f64 spheres only if they fit that
+        // too (config 2: 73.7 ms at five waves without them vs 75.8 at four with them; config 3:
+        // 89.8 vs 92.6); the others four, with up to 40 KB (the general instance at five: config
+        // 3 116.5 vs 100.6 ms).
         const size_t budget5 = 160 * 1024 / 5;
-        const bool w5 = W.sphere_only && kFiveWaves && std::getenv("CRT_FOUR_WAVES") == nullptr &&
+        const bool w5 = (W.sphere_only || W.quads_flat) && kFiveWaves && std::getenv("CRT_FOUR_WAVES") == nullptr &&
                         stack_at(scene_bytes) + stack_bytes + cam_bytes <= budget5;
         const size_t budget = w5 ? budget5 : kLdsSceneBudget;
         const uint32_t sph64 = static_cast<uint32_t>(s->spheres.size() * sizeof(DevSphere));
         if (W.spheres_f32 && kSph64Lds && stack_at(scene_bytes + sph64) + stack_bytes + cam_bytes <= budget)
             W.bytes_sph64 = sph64;
         W.lds_stack = stack_at(scene_bytes + W.bytes_sph64);
-        if (w5)
-            return launch_render<SE, false, true, false, true>(s, device, cam, W, W.lds_stack + stack_bytes, d_rgb, st, count_stats);
+        const size_t lds = W.lds_stack + stack_bytes;
         if (W.sphere_only)
-            return launch_render<SE, false, true, false>(s, device, cam, W, W.lds_stack + stack_bytes, d_rgb, st, count_stats);
-        return launch_render<SE, false, true, true>(s, device, cam, W, W.lds_stack + stack_bytes, d_rgb, st, count_stats);
+            return w5 ? launch_render<SE, false, true, 0, true>(s, device, cam, W, lds, d_rgb, st, count_stats)
+                      : launch_render<SE, false, true, 0, false>(s, device, cam, W, lds, d_rgb, st, count_stats);
+        if (W.quads_flat)
+            return w5 ? launch_render<SE, false, true, 2, true>(s, device, cam, W, lds, d_rgb, st, count_stats)
+                      : launch_render<SE, false, true, 2, false>(s, device, cam, W, lds, d_rgb, st, count_stats);
+        return launch_render<SE, false, true, 1>(s, device, cam, W, W.lds_stack + stack_bytes, d_rgb, st, count_stats);
     }
     // HBM scene: the top of the (breadth-first) node array goes to LDS as far as it fits beside
     // the stack without costing resident blocks (CRT_WAVES_PER_EU blocks of 4 waves, the VGPR
@@ -2386,13 +2391,13 @@ static int dispatch_render(const crt_scene* s, int device, const crt_camera* cam
         W.lds_nodes = 0;
         W.lds_stack = stack_at(align16(W.ntop));
         if (W.sphere_only)
-            return launch_render<SE, false, false, false>(s, device, cam, W, W.lds_stack + stack_bytes, d_rgb, st, count_stats);
-        return launch_render<SE, false, false, true>(s, device, cam, W, W.lds_stack + stack_bytes, d_rgb, st, count_stats);
+            return launch_render<SE, false, false, 0>(s, device, cam, W, W.lds_stack + stack_bytes, d_rgb, st, count_stats);
+        return launch_render<SE, false, false, 1>(s, device, cam, W, W.lds_stack + stack_bytes, d_rgb, st, count_stats);
     }
     W.ntop = top_bytes(per_block);
     W.lds_nodes = 0;
-    if (W.sphere_only) return launch_render<SE, true, false, false>(s, device, cam, W, W.ntop, d_rgb, st, count_stats);
-    return launch_render<SE, true, false, true>(s, device, cam, W, W.ntop, d_rgb, st, count_stats);
+    if (W.sphere_only) return launch_render<SE, true, false, 0>(s, device, cam, W, W.ntop, d_rgb, st, count_stats);
+    return launch_render<SE, true, false, 1>(s, device, cam, W, W.ntop, d_rgb, st, count_stats);
 }
 
 int device_render(const crt_scene* s, int device, const crt_camera* cam, const crt_tiling* t,

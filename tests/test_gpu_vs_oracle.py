@@ -298,11 +298,15 @@ def test_hbm_scene_kernels_with_parallelograms(crt, monkeypatch, name, kw, gstac
     check(gpu(crt, d, 60), orc.render(d, 60, threads=8))
 
 
-def test_five_wave_instance_equals_four_wave(crt, monkeypatch):
-    """Small sphere-only LDS scenes run the 5-wave instance (96 VGPRs, spills, no f64 spheres in
-    LDS); the 4-wave instance (CRT_FOUR_WAVES) gives the same frame bit for bit, and both the
-    oracle's."""
-    d = scene(crt, "rtow_final", 42, image_w=96, image_h=64, samples_per_pixel=8, max_depth=50)
+@pytest.mark.parametrize("name,seed,kw", [
+    ("rtow_final", 42, dict(image_w=96, image_h=64, samples_per_pixel=8, max_depth=50)),
+    ("cornell", None, dict(image_w=64, image_h=64, samples_per_pixel=8, max_depth=200)),
+])
+def test_five_wave_instance_equals_four_wave(crt, monkeypatch, name, seed, kw):
+    """Small sphere-only and flat-parallelogram LDS scenes run the 5-wave instances (96 VGPRs,
+    spills, no f64 spheres in LDS); the 4-wave instances (CRT_FOUR_WAVES) give the same frame bit
+    for bit, and both the oracle's."""
+    d = scene(crt, name, seed, **kw)
     five = gpu(crt, d, 70)
     check(five, orc.render(d, 70, threads=8))
     monkeypatch.setenv("CRT_FOUR_WAVES", "1")
