@@ -20,20 +20,27 @@ from pathlib import Path
 sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 from bench import kernel_source_sha  # noqa: E402
 
-KERNEL = "crt::dev::render_kernel<unsigned short, false, true, false, false>"  # sphere-only LDS scene, timed pass
+# the timed pass of an LDS-scene kernel (template: stack entry, GSTACK, LSCENE, COUNT = false, then the
+# primitive-mix and wave-count instance flags, which vary with the scene)
+KERNEL = "crt::dev::render_kernel<unsigned short, false, true, false,"
 
 
 def main():
     src, workload, out = Path(sys.argv[1]), sys.argv[2], Path(sys.argv[3])
     vals = defaultdict(list)
+    names = set()
     for f in sorted(src.glob("p*/run_counter_collection.csv")):
         for r in csv.DictReader(f.open()):
-            if r["Kernel_Name"].startswith("void " + KERNEL) or r["Kernel_Name"].startswith(KERNEL):
+            name = r["Kernel_Name"].removeprefix("void ")
+            if name.startswith(KERNEL):
                 vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
+                names.add(name.split("(")[0])
+    if len(names) > 1:
+        raise SystemExit(f"several timed kernel instances under {src}: {sorted(names)}")
     if not vals:
         raise SystemExit(f"no {KERNEL} rows under {src}")
     avg = {k: sum(v) / len(v) for k, v in vals.items()}
-    res = {"workload": workload, "kernel": KERNEL, "kernel_source_sha": kernel_source_sha(),
+    res = {"workload": workload, "kernel": names.pop(), "kernel_source_sha": kernel_source_sha(),
            "launches": {k: len(v) for k, v in vals.items()}}
     res.update({k: avg[k] for k in sorted(avg)})
     if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
