@@ -188,7 +188,58 @@ __device__ __forceinline__ uint32_t sample_seed(uint32_t base, uint32_t pixel, u
     return static_cast<uint32_t>(z ^ (z >> 32));
 }
 
+// sqrt(x) bit for bit for x in [2^-767, inf), given r = v_rsq_f64(x): hipcc's own gfx950
+// expansion of the IEEE sqrt (Goldschmidt + two Newton corrections) without its small-x scaling
+// and 0/inf fix-up, which are identities there. Outside that range: sqrt() itself.
+__device__ __forceinline__ double sqrt_from_rsq(double x, double r) {
+    if (__builtin_expect(!(x >= 0x1p-767 && x < __builtin_inf()), 0)) return sqrt(x);
+    double g = x * r, h = r * 0.5;
+    const double e = fma(-h, g, 0.5);
+    g = fma(g, e, g);
+    h = fma(h, e, h);
+    double d = fma(-g, g, x);
+    g = fma(d, h, g);
+    d = fma(-g, g, x);
+    return fma(d, h, g);
+}
+
+// The shading code's square roots and reciprocals (unit vectors, the Dielectric's sin and
+// refraction) without the range scaling and special-case fix-ups of hipcc's IEEE expansions, in
+// the five-wave sphere-only kernel instances (FAST; config 2 73.7 -> 73.1-73.4 ms); the others
+// keep sqrt() and the division (config 3 90.0 -> 91.3 ms, config 4 139.1 -> 140.2 ms with them).
+// CRT_EXACT_SHORTCUTS = 0: off everywhere.
+#ifndef CRT_EXACT_SHORTCUTS
+#define CRT_EXACT_SHORTCUTS 1
+#endif
+template <bool FAST>
+__device__ __forceinline__ double sqrt_exact(double x) {
+    if (FAST && CRT_EXACT_SHORTCUTS) return sqrt_from_rsq(x, __builtin_amdgcn_rsq(x));
+    return sqrt(x);
+}
+// 1 / s bit for bit: hipcc's gfx950 division 1 / s is div_scale, v_rcp_f64, two Newton steps
+// y = fma(y, fma(-s, y, 1), y), q = 1 * y, r = fma(-s, q, 1), div_fmas = fma(r, y, q), div_fixup.
+// For |s| in [2^-500, 2^500] div_scale scales nothing (it returns its operand), div_fmas adds no
+// scale and div_fixup returns its first operand (no NaN, inf, zero or denormal arises), so the
+// same operations without those three are that division's result; outside the range: 1 / s.
+__device__ __forceinline__ double recip_core(double s) {  // |s| in [2^-500, 2^500]
+#if CRT_EXACT_SHORTCUTS
+    double y = __builtin_amdgcn_rcp(s);
+    y = fma(y, fma(-s, y, 1.0), y);
+    y = fma(y, fma(-s, y, 1.0), y);
+    return fma(fma(-s, y, 1.0), y, y);
+#else
+    return 1 / s;
+#endif
+}
+template <bool FAST>
+__device__ __forceinline__ double recip_exact(double s) {
+    if (!FAST || !CRT_EXACT_SHORTCUTS) return 1 / s;
+    if (__builtin_expect(!(fabs(s) >= 0x1p-500 && fabs(s) <= 0x1p500), 0)) return 1 / s;
+    return recip_core(s);
+}
+
 // Vec3D::random_unit_vector (vec3d.h:64-75): rejection in the cube, then * (1 / |v|)
+template <bool FAST = false>
 __device__ __forceinline__ void random_unit_vector(uint32_t& s, double& x, double& y, double& z) {
     double m2;
 #if CRT_ABLATE_RUV  // timing experiment only (wrong results): one candidate, no rejection loop
@@ -204,7 +255,7 @@ __device__ __forceinline__ void random_unit_vector(uint32_t& s, double& x, doubl
         m2 = x * x + y * y + z * z;
     } while (!(m2 < 1));
 #endif
-    double inv = 1 / sqrt(x * x + y * y + z * z);
+    double inv = recip_exact<FAST>(sqrt_exact<FAST>(x * x + y * y + z * z));
     x = x * inv;
     y = y * inv;
     z = z * inv;
@@ -267,25 +318,11 @@ __device__ __forceinline__ bool slab(const NodeRegs& n, const double o[3], const
     return c1 & c2 & (xtmin < tmax) & (xtmax > tmin);
 }
 
-// sqrt(x) bit for bit for x in [2^-767, inf), given r = v_rsq_f64(x): hipcc's own gfx950
-// expansion of the IEEE sqrt (Goldschmidt + two Newton corrections) without its small-x scaling
-// and 0/inf fix-up, which are identities there. Outside that range: sqrt() itself.
-__device__ __forceinline__ double sqrt_from_rsq(double x, double r) {
-    if (__builtin_expect(!(x >= 0x1p-767 && x < __builtin_inf()), 0)) return sqrt(x);
-    double g = x * r, h = r * 0.5;
-    const double e = fma(-h, g, 0.5);
-    g = fma(g, e, g);
-    h = fma(h, e, h);
-    double d = fma(-g, g, x);
-    g = fma(d, h, g);
-    d = fma(-g, g, x);
-    return fma(d, h, g);
-}
-
 // Reciprocal of a ray's dot(d, d) for div_a: ia = RN(1 / a), or NaN when a is outside the range
 // where div_a's corrections are exact (then div_a divides).
+template <bool FAST = false>
 __device__ __forceinline__ double recip_a(double a) {
-    return (a >= 0x1p-500 && a <= 0x1p500) ? 1 / a : __builtin_nan("");
+    return (a >= 0x1p-500 && a <= 0x1p500) ? (FAST ? recip_core(a) : 1 / a) : __builtin_nan("");
 }
 
 // n / a correctly rounded from ia = RN(1/a): q0 = n * ia, then two residual corrections
@@ -1115,13 +1152,13 @@ __device__ __forceinline__ void walk(const SceneView& S, Stack<SE>& st, const do
 // the entered leaf's primitives in order (bvh.h:635-652), then "return" to the DFS.
 // Sphere-only scenes store spheres in slot order, so the slot indexes them directly and the next
 // sphere is loaded while the current one is tested.
-template <typename SE, bool COUNT, bool TOP, bool LS>
+template <typename SE, bool COUNT, bool TOP, bool LS, bool FAST = false>
 __device__ __forceinline__ void leaf_step(const SceneView& S, Stack<SE>& st, const double o[3],
                                           const double d[3], double tmin, float tmin32, bool sphere_only, bool pairs,
                                           bool qfilter, bool qflat, Trav& R, LaneCounters& ctr) {
     const uint2 range = make_uint2(R.first, R.count);  // index, count
     const uint32_t end = range.x + range.y;
-    const double ia = recip_a(R.a), lo = lim_tmin(tmin, R.a);
+    const double ia = recip_a<FAST>(R.a), lo = lim_tmin(tmin, R.a);
     double hi = lim_tmax(R.tmax, R.a);
     if (pairs && range.y <= 32 && leaf_ray32_ok(o, d, R.a)) {
         // two passes: the packed f32 candidate filter over every sphere against the leaf-entry
@@ -1348,7 +1385,7 @@ __device__ __forceinline__ void start_path(const CamView& C, uint32_t row, uint3
 // One level of ray_color (camera.h:205-258) after the closest-hit query: scatters
 // (material.h:64-263) into the next ray, or ends the path adding T * (background | emission) to
 // acc. Returns true when the path has ended (miss, light, absorption).
-template <bool LS, bool SPH = false, bool QONLY = false>
+template <bool LS, bool SPH = false, bool QONLY = false, bool FAST = false>
 __device__ __forceinline__ bool shade(const SceneView& S, const CamView& C, Path& P, bool hit,
                                       uint32_t ref, double t, double acc[3]) {
     if (!hit) {
@@ -1378,7 +1415,7 @@ __device__ __forceinline__ bool shade(const SceneView& S, const CamView& C, Path
     // order (no lane draws in two of these steps).
     double ux0 = 0, uy0 = 0, uz0 = 0;
     if (met || die) {
-        const double il = 1 / sqrt(P.d[0] * P.d[0] + P.d[1] * P.d[1] + P.d[2] * P.d[2]);
+        const double il = recip_exact<FAST>(sqrt_exact<FAST>(P.d[0] * P.d[0] + P.d[1] * P.d[1] + P.d[2] * P.d[2]));
         ux0 = P.d[0] * il;
         uy0 = P.d[1] * il;
         uz0 = P.d[2] * il;
@@ -1388,7 +1425,7 @@ __device__ __forceinline__ bool shade(const SceneView& S, const CamView& C, Path
     if (die) {  // material.h:185-218, vec3d.h:168-200
         ratio = front ? M.color[0] : M.param;  // 1. / ri, ri / 1. (precomputed: upload)
         cosv = fmin((-ux0) * n[0] + (-uy0) * n[1] + (-uz0) * n[2], 1.);
-        const double sinv = sqrt(1 - cosv * cosv);
+        const double sinv = sqrt_exact<FAST>(1 - cosv * cosv);
         if (ratio * sinv > 1) {
             reflect = true;  // total internal reflection, no draw
         } else {
@@ -1398,7 +1435,7 @@ __device__ __forceinline__ bool shade(const SceneView& S, const CamView& C, Path
         }
     }
     double rx = 0, ry = 0, rz = 0;
-    if (lam || met) random_unit_vector(P.rng, rx, ry, rz);
+    if (lam || met) random_unit_vector<FAST>(P.rng, rx, ry, rz);
     double nd[3];
     if (reflect) {  // Metal (material.h:116-139) or a reflecting Dielectric
         const double k2 = 2 * (ux0 * n[0] + uy0 * n[1] + uz0 * n[2]);
@@ -1415,7 +1452,7 @@ __device__ __forceinline__ bool shade(const SceneView& S, const CamView& C, Path
         const double px = (ux0 + n[0] * cosv) * ratio;
         const double py = (uy0 + n[1] * cosv) * ratio;
         const double pz = (uz0 + n[2] * cosv) * ratio;
-        const double sq = -sqrt(fabs(1 - (px * px + py * py + pz * pz)));
+        const double sq = -sqrt_exact<FAST>(fabs(1 - (px * px + py * py + pz * pz)));
         nd[0] = px + n[0] * sq;
         nd[1] = py + n[1] * sq;
         nd[2] = pz + n[2] * sq;
@@ -1540,6 +1577,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W5 ? 5 :
     // the instances with PM = 0 are launched for sphere-only scenes only, PM = 2 for scenes of
     // axis-aligned parallelograms only: the other primitive's paths are compiled out of them
     constexpr bool kSphOnly = PM == 0, kFlatOnly = PM == 2;
+    // sqrt / reciprocal expansions without range fix-ups (sqrt_exact, recip_exact): measured
+    // faster only in the five-wave sphere-only instance
+    constexpr bool kFast = kSphOnly && W5;
     SceneView S = Sg;
     if (LSCENE) {  // f32 nodes at LDS offset 0 (fetch_nodef: a node's LDS address is its ref)
         if (static_cast<uint32_t>(reinterpret_cast<uintptr_t>((LdsByte*)smem)) != 0) __builtin_trap();
@@ -1725,7 +1765,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W5 ? 5 :
                 if (wave_leader()) atomicAdd(&counters->round_leaves, nl);
             }
             if (COUNT) cl -= static_cast<uint32_t>(wall_clock64());
-            if (R.state == kLeaf) leaf_step<SE, COUNT, kTopTreelet && !LSCENE, LSCENE>(S, st, P.o, P.d, C.t_min, tmin32, kSphOnly || (!kFlatOnly && W.sphere_only != 0), !kFlatOnly && W.spheres_f32 != 0, kFlatOnly || (!kSphOnly && W.quads_f32 != 0), kFlatOnly || (!kSphOnly && W.quads_flat != 0), R, ctr);
+            if (R.state == kLeaf) leaf_step<SE, COUNT, kTopTreelet && !LSCENE, LSCENE, kFast>(S, st, P.o, P.d, C.t_min, tmin32, kSphOnly || (!kFlatOnly && W.sphere_only != 0), !kFlatOnly && W.spheres_f32 != 0, kFlatOnly || (!kSphOnly && W.quads_f32 != 0), kFlatOnly || (!kSphOnly && W.quads_flat != 0), R, ctr);
             if (COUNT) cl += static_cast<uint32_t>(wall_clock64());
             const uint64_t pending = __ballot(R.state == kWalk);
             const uint64_t finished = __ballot(R.state == kDone);
@@ -1744,7 +1784,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W5 ? 5 :
             flush_counts(ctr, counters);
         if (R.state == kDone) {
             if (COUNT && wave_leader()) ctr.it_shade++;
-            bool ended = shade<LSCENE, kSphOnly, kFlatOnly>(S, CL, P, R.found, R.ref, R.tmax, acc);
+            bool ended = shade<LSCENE, kSphOnly, kFlatOnly, kFast>(S, CL, P, R.found, R.ref, R.tmax, acc);
             // a scattered ray with no bounce left returns RGB::zero() (camera.h:211-213)
             if (!ended && P.depth == 0) ended = true;
             if (!ended) {
