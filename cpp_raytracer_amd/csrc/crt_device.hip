@@ -1400,7 +1400,11 @@ __device__ __forceinline__ bool shade(const SceneView& S, const CamView& C, Path
     bool front;
     (void)hit_record<LS, true, SPH, QONLY>(S, ref, P.o, P.d, t, p, n, front, M.emit[0]);
     const uint32_t kind = M.kind;
+#if CRT_ABLATE_MAT  // timing experiment only (wrong results): every scattering material as Lambertian
+    const bool lam = kind == CRT_LAMBERTIAN || kind == CRT_METAL || kind == CRT_DIELECTRIC, met = false, die = false;
+#else
     const bool lam = kind == CRT_LAMBERTIAN, met = kind == CRT_METAL, die = kind == CRT_DIELECTRIC;
+#endif
     if (!(lam || met || die)) {  // DiffuseLight: emits, never scatters (material.h:248-263)
         acc[0] = acc[0] + P.T[0] * M.emit[0];
         acc[1] = acc[1] + P.T[1] * M.emit[1];
