@@ -178,6 +178,17 @@ __device__ __forceinline__ double rnd(uint32_t& s, double lo, double hi) {
     s = 1664525u * s + 1013904223u;
     return lo + (hi - lo) * static_cast<double>(s) * kScale;
 }
+// rnd(s, -1, 1) and rnd(s, 0, 1) with one f64 operation fewer, bit for bit: (1 - -1) * x = 2x is
+// exact (x < 2^32), and RN(2x * kScale) = RN(x * (2 kScale)) with 2 kScale exact; 0 + y = y for
+// the y = RN(x * kScale) >= 0 here (+0 included)
+__device__ __forceinline__ double rnd_pm1(uint32_t& s) {
+    s = 1664525u * s + 1013904223u;
+    return static_cast<double>(s) * (2 * kScale) + -1.0;
+}
+__device__ __forceinline__ double rnd_01(uint32_t& s) {
+    s = 1664525u * s + 1013904223u;
+    return static_cast<double>(s) * kScale;
+}
 
 __device__ __forceinline__ uint32_t sample_seed(uint32_t base, uint32_t pixel, uint32_t sample) {
     uint64_t z = (static_cast<uint64_t>(pixel) << 32) | sample;
@@ -243,15 +254,15 @@ template <bool FAST = false>
 __device__ __forceinline__ void random_unit_vector(uint32_t& s, double& x, double& y, double& z) {
     double m2;
 #if CRT_ABLATE_RUV  // timing experiment only (wrong results): one candidate, no rejection loop
-    x = rnd(s, -1, 1);
-    y = rnd(s, -1, 1);
-    z = rnd(s, -1, 1);
+    x = rnd_pm1(s);
+    y = rnd_pm1(s);
+    z = rnd_pm1(s);
     m2 = x * x + y * y + z * z;
 #else
     do {
-        x = rnd(s, -1, 1);
-        y = rnd(s, -1, 1);
-        z = rnd(s, -1, 1);
+        x = rnd_pm1(s);
+        y = rnd_pm1(s);
+        z = rnd_pm1(s);
         m2 = x * x + y * y + z * z;
     } while (!(m2 < 1));
 #endif
@@ -1351,12 +1362,12 @@ __device__ __forceinline__ void start_path(const CamView& C, uint32_t row, uint3
     } else {  // random_point_in_defocus_disk (camera.h:160-168, vec3d.h:79-85)
         double vx, vy;
 #if CRT_ABLATE_DISK  // timing experiment only (wrong results): one candidate
-        vx = rnd(rng, -1, 1);
-        vy = rnd(rng, -1, 1);
+        vx = rnd_pm1(rng);
+        vy = rnd_pm1(rng);
 #else
         do {
-            vx = rnd(rng, -1, 1);
-            vy = rnd(rng, -1, 1);
+            vx = rnd_pm1(rng);
+            vy = rnd_pm1(rng);
         } while (!(vx * vx + vy * vy + 0.0 * 0.0 < 1));
 #endif
         P.o[0] = (C.o[0] + C.ddx[0] * vx) + C.ddy[0] * vy;
@@ -1435,7 +1446,7 @@ __device__ __forceinline__ bool shade(const SceneView& S, const CamView& C, Path
         } else {
             const double r0 = front ? M.color[1] : M.color[2];  // reflectance's r0 (upload)
             const double refl = r0 + (1 - r0) * pow5(1 - cosv);
-            reflect = rnd(P.rng, 0, 1) < refl;
+            reflect = rnd_01(P.rng) < refl;
         }
     }
     double rx = 0, ry = 0, rz = 0;
