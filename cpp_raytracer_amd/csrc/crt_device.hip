@@ -50,6 +50,10 @@ constexpr uint32_t kTileW = CRT_TILE_W, kTileH = 64 / CRT_TILE_W;
 #ifndef CRT_SPEC_MASKED
 #define CRT_SPEC_MASKED 1
 #endif
+// the five-wave sphere-only instance keeps the lanes' pixel sums in LDS (render_kernel: kAccLds)
+#ifndef CRT_ACC_LDS
+#define CRT_ACC_LDS 1
+#endif
 constexpr double kScale = 1 / static_cast<double>(4294967295u - 1);  // rand_util.h:110-112
 
 typedef double Dvec2 __attribute__((ext_vector_type(2)));
@@ -118,6 +122,7 @@ struct Work {
     uint32_t ntop;          // HBM-scene kernels: f32 nodes [0, ntop) bytes staged in LDS at offset 0
     uint32_t sentinel;      // the sentinel node's reference (byte offset into the f32 nodes)
     uint32_t lds_cam;       // LDS copy of the CamView (read where used: keeps it out of SGPRs)
+    uint32_t lds_acc;       // five-wave instances: the lanes' pixel sums (3 x kBlock doubles)
     uint32_t f32_ok;        // node bounds fit the f32 walk's error analysis (else f64 decides)
     uint32_t spheres_f32;   // sphere-only scene within the f32 filter's range (two-pass leaves)
     uint32_t quads_f32;     // parallelogram-only scene within its f32 filter's range (two-pass leaves)
@@ -1657,6 +1662,19 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W5 ? 5 :
     // the lane's unit: tile (tx | ty << 16), chunk << 6 | tile pixel; and its current sample
     uint32_t u_txy = 0, u_cp = 0, s = 0;
     double acc[3] = {0, 0, 0};
+    // the five-wave sphere-only instance: the pixel sum lives in LDS (three doubles a lane,
+    // [k][lane]), not in six VGPRs live across every phase (spill stores 17 -> 9; config 2 73.1-73.4
+    // -> 72.6 ms, config 3 0.4% slower with it in the flat instance); shade adds a path's
+    // contribution to a zeroed local (0 + x = x) that then goes into the LDS sum: the same
+    // additions as acc + x
+    constexpr bool kAccLds = kFast && CRT_ACC_LDS;
+    typedef __attribute__((address_space(3))) double LdsDouble;
+    LdsDouble* const acc_l = (LdsDouble*)static_cast<uintptr_t>(W.lds_acc + threadIdx.x * 8);
+    if (kAccLds) {
+        acc_l[0] = 0;
+        acc_l[kBlock] = 0;
+        acc_l[2 * kBlock] = 0;
+    }
     Path P;
     Trav R;
     R.state = kIdle;
@@ -1799,7 +1817,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W5 ? 5 :
             flush_counts(ctr, counters);
         if (R.state == kDone) {
             if (COUNT && wave_leader()) ctr.it_shade++;
-            bool ended = shade<LSCENE, kSphOnly, kFlatOnly, kFast>(S, CL, P, R.found, R.ref, R.tmax, acc);
+            double contrib[3] = {0, 0, 0};
+            bool ended = shade<LSCENE, kSphOnly, kFlatOnly, kFast>(S, CL, P, R.found, R.ref, R.tmax, kAccLds ? contrib : acc);
+            if (kAccLds && ended) {
+                acc_l[0] = acc_l[0] + contrib[0];
+                acc_l[kBlock] = acc_l[kBlock] + contrib[1];
+                acc_l[2 * kBlock] = acc_l[2 * kBlock] + contrib[2];
+            }
             // a scattered ray with no bounce left returns RGB::zero() (camera.h:211-213)
             if (!ended && P.depth == 0) ended = true;
             if (!ended) {
@@ -1814,9 +1838,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W5 ? 5 :
                         const uint32_t col = (u_txy & 0xffffu) * kTileW + pix % kTileW, k = (u_txy >> 16) * kTileH + pix / kTileW;
                         double* dst = partial + (static_cast<size_t>(chunk) * W.bh * W.bw +
                                                  static_cast<size_t>(k) * W.bw + col) * 3;
-                        dst[0] = acc[0];
-                        dst[1] = acc[1];
-                        dst[2] = acc[2];
+                        dst[0] = kAccLds ? acc_l[0] : acc[0];
+                        dst[1] = kAccLds ? acc_l[kBlock] : acc[1];
+                        dst[2] = kAccLds ? acc_l[2 * kBlock] : acc[2];
+                    }
+                    if (kAccLds) {
+                        acc_l[0] = 0;
+                        acc_l[kBlock] = 0;
+                        acc_l[2 * kBlock] = 0;
                     }
                     acc[0] = 0;
                     acc[1] = 0;
@@ -2177,6 +2206,7 @@ static uint32_t count_owned(uint32_t h, uint32_t rb, uint32_t tc, uint32_t ti) {
 
 static size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
 
+constexpr size_t kAccBytes = CRT_ACC_LDS ? 3 * dev::kBlock * sizeof(double) : 0;  // five-wave sphere-only pixel sums
 #ifndef CRT_FIVE_WAVES
 #define CRT_FIVE_WAVES 1
 #endif
@@ -2210,6 +2240,10 @@ static int launch_render(const crt_scene* s, int device, const crt_camera* cam, 
     dev::Work W = w0;
     W.lds_cam = static_cast<uint32_t>(align16(lds));  // the camera copy after the rest
     lds = W.lds_cam + align16(sizeof(dev::CamView));
+    if (W5 && PM == 0 && CRT_ACC_LDS) {  // then the pixel sums (render_kernel: kAccLds)
+        W.lds_acc = static_cast<uint32_t>(align16(lds));
+        lds = W.lds_acc + kAccBytes;
+    }
     const uint64_t pixels = static_cast<uint64_t>(W.owned_rows) * cam->image_w;
     // Sample chunks: a function of spp ONLY, so every pixel's sum is grouped identically whatever
     // the tiling / number of GPUs / lane schedule / band split (bit-identical frames for 1..N
@@ -2416,10 +2450,10 @@ static int dispatch_render(const crt_scene* s, int device, const crt_camera* cam
         // 3 116.5 vs 100.6 ms).
         const size_t budget5 = 160 * 1024 / 5;
         const bool w5 = (W.sphere_only || W.quads_flat) && kFiveWaves && std::getenv("CRT_FOUR_WAVES") == nullptr &&
-                        stack_at(scene_bytes) + stack_bytes + cam_bytes <= budget5;
+                        stack_at(scene_bytes) + stack_bytes + cam_bytes + (W.sphere_only ? kAccBytes : 0) <= budget5;
         const size_t budget = w5 ? budget5 : kLdsSceneBudget;
         const uint32_t sph64 = static_cast<uint32_t>(s->spheres.size() * sizeof(DevSphere));
-        if (W.spheres_f32 && kSph64Lds && stack_at(scene_bytes + sph64) + stack_bytes + cam_bytes <= budget)
+        if (W.spheres_f32 && kSph64Lds && stack_at(scene_bytes + sph64) + stack_bytes + cam_bytes + (w5 ? kAccBytes : 0) <= budget)
             W.bytes_sph64 = sph64;
         W.lds_stack = stack_at(scene_bytes + W.bytes_sph64);
         const size_t lds = W.lds_stack + stack_bytes;
