@@ -54,6 +54,10 @@ constexpr uint32_t kTileW = CRT_TILE_W, kTileH = 64 / CRT_TILE_W;
 #ifndef CRT_ACC_LDS
 #define CRT_ACC_LDS 1
 #endif
+// waves per SIMD of the W5 instances (the "five-wave" ones)
+#ifndef CRT_MANY_WAVES
+#define CRT_MANY_WAVES 5
+#endif
 constexpr double kScale = 1 / static_cast<double>(4294967295u - 1);  // rand_util.h:110-112
 
 typedef double Dvec2 __attribute__((ext_vector_type(2)));
@@ -1590,7 +1594,7 @@ constexpr bool kRoundCounters = CRT_ROUND_COUNTERS != 0;
 // W5: 5 waves per SIMD (96 VGPRs, ~40-48 of them spilled), launched for sphere-only and
 // flat-parallelogram LDS scenes whose LDS copy leaves room for five blocks per CU (dispatch_render)
 template <typename SE, bool GSTACK, bool LSCENE, bool COUNT, int PM, bool W5>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W5 ? 5 : LSCENE ? CRT_WAVES_PER_EU_LDS : CRT_WAVES_PER_EU, 8))) void render_kernel(
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W5 ? CRT_MANY_WAVES : LSCENE ? CRT_WAVES_PER_EU_LDS : CRT_WAVES_PER_EU, 8))) void render_kernel(
     SceneView Sg, CamView C, Work W, double* __restrict__ partial, SE* __restrict__ gstack,
     Counters* __restrict__ counters) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -2448,7 +2452,7 @@ static int dispatch_render(const crt_scene* s, int device, const crt_camera* cam
         // too (config 2: 73.7 ms at five waves without them vs 75.8 at four with them; config 3:
         // 89.8 vs 92.6); the others four, with up to 40 KB (the general instance at five: config
         // 3 116.5 vs 100.6 ms).
-        const size_t budget5 = 160 * 1024 / 5;
+        const size_t budget5 = 160 * 1024 / CRT_MANY_WAVES;  // blocks of four waves a CU
         const bool w5 = (W.sphere_only || W.quads_flat) && kFiveWaves && std::getenv("CRT_FOUR_WAVES") == nullptr &&
                         stack_at(scene_bytes) + stack_bytes + cam_bytes + (W.sphere_only ? kAccBytes : 0) <= budget5;
         const size_t budget = w5 ? budget5 : kLdsSceneBudget;
