@@ -10,6 +10,13 @@
  *                                        (camera.h:279-293 loop, reference random_ray_through_pixel
  *                                        and ray_color; state injected per (pixel, sample))
  *   samples <scene> <base> <out> r0 r1 c0 c1   per-sample RGB of the same crop
+ *   render_linear <scene> <base> <out> [r0 r1 c0 c1]
+ *                                        the same render with the Scene itself as the world:
+ *                                        ray_color<Scene> -> Scene::hit_by (scene.h:59-75) and
+ *                                        Box::hit_by (box.h:24-28), no BVH (camera.h:264-297)
+ *   render_nested <scene> <base> <out> <group> [r0 r1 c0 c1]
+ *                                        as render_linear, with the objects regrouped into nested
+ *                                        Scenes (runs of <group> objects, pairs of those again)
  *   hits    <scene> <rays> <out>         BVH::hit_by closest hits          (bvh.h:585-715)
  *   time    <scene> <threads> [rows]     unmodified Camera::render timing  (CPU baseline)
  *   refsum  <scene> <seed>               1-thread unmodified render checksum (shim check)
@@ -164,12 +171,13 @@ static void write_npy(const char* path, const std::vector<double>& data, std::ve
 }
 
 #ifdef CRT_ORACLE_SHIM
-// per-sample-seeded render of rows [r0,r1) x cols [c0,c1); samples != null -> per-sample RGB
-static void render_crop(Loaded& L, uint32_t base, size_t r0, size_t r1, size_t c0, size_t c1,
-                        std::vector<double>& out, std::vector<double>* samples) {
+// per-sample-seeded render of rows [r0,r1) x cols [c0,c1) of `world` (a BVH, or a Scene for the
+// generic render<T>); samples != null -> per-sample RGB
+template <typename World>
+static void render_crop(Loaded& L, const World& bvh, uint32_t base, size_t r0, size_t r1, size_t c0,
+                        size_t c1, std::vector<double>& out, std::vector<double>* samples) {
     Camera cam = make_camera(L.cs);
     cam.init();
-    BVH bvh(L.world);
     const size_t w = c1 - c0, spp = cam.samples_per_pixel;
     out.assign((r1 - r0) * w * 3, 0.0);
     if (samples) samples->assign((r1 - r0) * w * spp * 3, 0.0);
@@ -262,16 +270,40 @@ int main(int argc, char** argv) {
         return 0;
     }
 #ifdef CRT_ORACLE_SHIM
-    if (mode == "render" || mode == "samples") {
+    if (mode == "render" || mode == "samples" || mode == "render_linear" || mode == "render_nested") {
         uint32_t base = static_cast<uint32_t>(std::strtoul(argv[3], nullptr, 10));
+        const int a = mode == "render_nested" ? 6 : 5;  // first crop argument
+        if (mode == "render_nested" && argc < 6) return 2;
         size_t r0 = 0, r1 = L.cs.h, c0 = 0, c1 = L.cs.w;
-        if (argc >= 9) {
-            r0 = std::strtoul(argv[5], nullptr, 10); r1 = std::strtoul(argv[6], nullptr, 10);
-            c0 = std::strtoul(argv[7], nullptr, 10); c1 = std::strtoul(argv[8], nullptr, 10);
+        if (argc >= a + 4) {
+            r0 = std::strtoul(argv[a], nullptr, 10); r1 = std::strtoul(argv[a + 1], nullptr, 10);
+            c0 = std::strtoul(argv[a + 2], nullptr, 10); c1 = std::strtoul(argv[a + 3], nullptr, 10);
         }
         std::vector<double> out, smp;
-        render_crop(L, base, r0, r1, c0, c1, out, mode == "samples" ? &smp : nullptr);
-        if (mode == "render") write_npy(argv[4], out, {r1 - r0, c1 - c0, 3});
+        if (mode == "render_linear") {
+            render_crop(L, L.world, base, r0, r1, c0, c1, out, nullptr);
+        } else if (mode == "render_nested") {
+            // runs of `group` objects become inner Scenes, pairs of inner Scenes middle Scenes
+            const size_t group = std::max<size_t>(1, std::strtoul(argv[5], nullptr, 10));
+            Scene outer, mid;
+            std::shared_ptr<Scene> inner;
+            size_t n_inner = 0, i = 0;
+            for (const auto& o : L.world) {
+                if (i++ % group == 0) {
+                    if (inner) { mid.add(inner); ++n_inner; }
+                    if (n_inner == 2) { outer.add(std::make_shared<Scene>(mid)); mid = Scene(); n_inner = 0; }
+                    inner = std::make_shared<Scene>();
+                }
+                inner->add(o);
+            }
+            if (inner) mid.add(inner);
+            if (mid.size()) outer.add(std::make_shared<Scene>(mid));
+            render_crop(L, outer, base, r0, r1, c0, c1, out, nullptr);
+        } else {
+            BVH bvh(L.world);
+            render_crop(L, bvh, base, r0, r1, c0, c1, out, mode == "samples" ? &smp : nullptr);
+        }
+        if (mode != "samples") write_npy(argv[4], out, {r1 - r0, c1 - c0, 3});
         else write_npy(argv[4], smp, {r1 - r0, c1 - c0, L.cs.spp, 3});
         return 0;
     }

@@ -53,6 +53,16 @@ SAMPLE_CASES = [
     ("cornell_samples", "cornell", None, dict(image_w=600, image_h=600, samples_per_pixel=16, max_depth=1000),
      22, (296, 304, 296, 304)),
 ]
+# the generic render<T> with the Scene itself as the world (Scene::hit_by / Box::hit_by, no BVH):
+# (case, scene, seed, camera overrides, base_seed, crop, nesting group or None)
+LINEAR_CASES = [
+    ("cornell_linear", "cornell", None, dict(image_w=600, image_h=600, samples_per_pixel=8, max_depth=1000),
+     18, (250, 282, 200, 264), None),
+    ("lights_nested", "rtow_final_lights", None, dict(image_w=400, image_h=225, samples_per_pixel=8),
+     19, (80, 112, 180, 244), 7),
+    ("boxes_nested", "cornell", None, dict(image_w=96, image_h=96, samples_per_pixel=6, max_depth=200),
+     20, None, 3),
+]
 BVH_SCENES = [("config1", None), ("rtow_final", 42), ("cornell", None), ("parallelograms", None),
               ("christmas_tree", None), ("bvh_pathological", None), ("rtow_final_lights", None)]
 HIT_SCENES = [("rtow_final", 42, 4096), ("cornell", None, 4096), ("christmas_tree", None, 2048)]
@@ -164,6 +174,22 @@ def gen_ppm(tmp: Path) -> None:
     np.savez_compressed(GOLD / "ppm_cases.npz", **out)
 
 
+def gen_linear(tmp: Path, meta: dict) -> None:
+    """Renders of the Scene itself (oracle/_ref render_linear / render_nested modes)."""
+    for case, name, seed, ov, base, crop, group in LINEAR_CASES:
+        p, d = scene_file(tmp, name, seed, ov)
+        out = tmp / "l.npy"
+        if group is None:
+            run("render_linear", p, base, out, *(crop or ()))
+        else:
+            run("render_nested", p, base, out, group, *(crop or ()))
+        rgb = np.load(out)
+        np.savez_compressed(GOLD / f"render_{case}.npz", rgb=rgb)
+        meta["renders"][case] = {"scene": name, "seed": seed, "camera": ov, "base_seed": base,
+                                 "crop": crop, "shape": list(rgb.shape), "world": "scene" if group is None
+                                 else f"nested scenes (group {group})"}
+
+
 def main() -> None:
     subprocess.run(["make", "-C", str(ROOT / "oracle"), "ref"], check=True)
     meta = {"generator": "tests/golden/gen_golden.py", "reference": "DeltaPavonis/cpp_raytracer (oracle/_ref)",
@@ -223,6 +249,7 @@ def main() -> None:
             out = tmp / "h.npy"
             run("hits", p, rays_path, out)
             np.savez_compressed(GOLD / f"hits_{name}.npz", rays=rays, hits=np.load(out))
+        gen_linear(tmp, meta)
         gen_ppm(tmp)
         gen_bvh_ties(tmp)
     (GOLD / "golden.json").write_text(json.dumps(meta, indent=1, sort_keys=True))
@@ -230,7 +257,13 @@ def main() -> None:
 
 
 if __name__ == "__main__":
-    if sys.argv[1:] in (["ppm"], ["ties"]):  # only the PPM-value / tie-BVH fixtures
+    if sys.argv[1:] == ["linear"]:  # only the linear-world renders, merged into golden.json
+        subprocess.run(["make", "-C", str(ROOT / "oracle"), "ref"], check=True)
+        m = json.loads((GOLD / "golden.json").read_text())
+        with tempfile.TemporaryDirectory() as td:
+            gen_linear(Path(td), m)
+        (GOLD / "golden.json").write_text(json.dumps(m, indent=1, sort_keys=True))
+    elif sys.argv[1:] in (["ppm"], ["ties"]):  # only the PPM-value / tie-BVH fixtures
         subprocess.run(["make", "-C", str(ROOT / "oracle"), "ref"], check=True)
         with tempfile.TemporaryDirectory() as td:
             (gen_ppm if sys.argv[1] == "ppm" else gen_bvh_ties)(Path(td))

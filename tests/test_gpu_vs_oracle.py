@@ -58,7 +58,8 @@ def test_hbm_stack_variant(crt, monkeypatch):
 
 
 def test_linear_mode_matches_bvh(crt):
-    # a non-Scene Hittable renders through one always-entered leaf; same pixels as the BVH
+    # a non-Scene Hittable renders through one always-entered leaf; same pixels as the BVH (the
+    # reference-pinned linear cases are test_gpu_parity.py::test_linear_world_matches_reference)
     d = scene(crt, "cornell", image_w=48, image_h=48, samples_per_pixel=4, max_depth=50)
     check(gpu(crt, d, 35, linear=True), gpu(crt, d, 35))
 

@@ -88,3 +88,31 @@ def test_oracle_bvh_matches_library_on_big_scene(crt):
     ln, lo = crt.GpuScene(d).export_bvh()
     assert hashlib.sha256(on.tobytes()).digest() == hashlib.sha256(ln.tobytes()).digest()
     assert np.array_equal(oo, lo)
+
+
+REF_DIR = ROOT / "oracle" / "_ref"
+
+
+@pytest.mark.skipif(not (REF_DIR / "ref_driver").exists() or not (REF_DIR / "ref_driver_plain").exists(),
+                    reason="oracle/_ref not built (needs /root/reference)")
+@pytest.mark.parametrize("name,overrides,seed,want", [
+    ("config1", {}, 12345, "127063.74069625582"),   # SURVEY 8c probe: 127063.740696255816
+    ("cornell", dict(image_w=100, image_h=100, samples_per_pixel=4, max_depth=50), 7, None),
+    ("rtow_final", dict(image_w=60, image_h=40, samples_per_pixel=4, max_depth=50), 3, None),
+])
+def test_shim_matches_plain_reference(crt, tmp_path, name, overrides, seed, want):
+    """The RNG shim (oracle/ref_shim/util/rand_util.h) every render golden rests on changes nothing
+    without state injection: the shim build and the build against the reference's own
+    rand_util.h render the same single-threaded unmodified Camera::render to the same RGB sum
+    (`make -C oracle check-shim`)."""
+    import subprocess
+    from cpp_raytracer_amd import camera_with
+    d = crt.SceneData.named(name, 42 if name == "rtow_final" else None)
+    d.camera = camera_with(d.camera, **overrides)
+    p = tmp_path / "s.crts"
+    d.save(p)
+    sums = [subprocess.run([str(REF_DIR / b), "refsum", str(p), str(seed)], capture_output=True, text=True,
+                           check=True, timeout=120).stdout.strip() for b in ("ref_driver", "ref_driver_plain")]
+    assert sums[0] == sums[1]
+    if want is not None:
+        assert sums[0] == want
