@@ -209,6 +209,13 @@ class GpuScene:
               "crt_render")
         return out, st
 
+    def guard(self, device: int = 0, reset: bool = False) -> int:
+        """Dielectric decisions since upload (or the last reset) that a one-ulp different
+        pow(1 - cos, 5) could have flipped (crt_render_guard; 0 = every branch as the reference's)."""
+        v = C.c_uint64()
+        check(lib().crt_render_guard(self._h, device, C.byref(v), int(reset)), "crt_render_guard")
+        return int(v.value)
+
     def closest_hits(self, rays: np.ndarray, t_min: float = 1e-5, t_max: float = float("inf"),
                      device: int = 0) -> np.ndarray:
         rays = np.ascontiguousarray(rays, np.float64).reshape(-1, 6)

@@ -123,6 +123,7 @@ EXPORTS = {
                                    C.c_void_p]),
     "crt_ppm_values": (C.c_int, [C.c_int, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p]),
     "crt_ppm_write": (C.c_int, [C.c_char_p, C.c_uint32, C.c_uint32, C.c_void_p]),
+    "crt_render_guard": (C.c_int, [C.c_void_p, C.c_int, P(C.c_uint64), C.c_int]),
 }
 
 

@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "crt_internal.h"
+#include "crt_schlick.h"
 
 #pragma clang fp contract(off)
 
@@ -83,6 +84,7 @@ struct SceneView {
     // LSCENE kernels: LDS byte offsets of the staged refs / f64 spheres / parallelograms, read
     // through typed LDS pointers (ds_read, not flat); spheres_lds = ~0u when the spheres stay in HBM
     uint32_t refs_lds, spheres_lds, quads_lds;
+    unsigned long long* guard;   // parity guard words (DeviceCopy::guard)
 };
 
 struct CamView {
@@ -279,17 +281,6 @@ __device__ __forceinline__ void random_unit_vector(uint32_t& s, double& x, doubl
     x = x * inv;
     y = y * inv;
     z = z * inv;
-}
-
-// x^5 rounded once from a double-double product (std::pow(1 - cos, 5), material.h:180)
-__device__ __forceinline__ double pow5(double x) {
-    double x2h = x * x;
-    double x2l = __builtin_fma(x, x, -x2h);
-    double x4h = x2h * x2h;
-    double x4l = __builtin_fma(x2h, x2h, -x4h) + 2 * x2h * x2l;
-    double x5h = x4h * x;
-    double x5l = __builtin_fma(x4h, x, -x5h) + x4l * x;
-    return x5h + x5l;
 }
 
 // AABB::is_hit_by_optimized (aabb.h:132-174). The early returns of the reference are folded into
@@ -1454,8 +1445,12 @@ __device__ __forceinline__ bool shade(const SceneView& S, const CamView& C, Path
             reflect = true;  // total internal reflection, no draw
         } else {
             const double r0 = front ? M.color[1] : M.color[2];  // reflectance's r0 (upload)
-            const double refl = r0 + (1 - r0) * pow5(1 - cosv);
-            reflect = rnd_01(P.rng) < refl;
+            const double pw = pow5(1 - cosv);
+            const double u = rnd_01(P.rng);
+            reflect = u < r0 + (1 - r0) * pw;
+            // a branch a 1-ulp different pow could flip (crt_schlick.h): counted, never taken in
+            // practice (probability ~2^-50 per decision)
+            if (__builtin_expect(schlick_undecided(u, r0, pw), 0)) atomicAdd(S.guard, 1ull);
         }
     }
     double rx = 0, ry = 0, rz = 0;
@@ -1975,8 +1970,10 @@ __global__ __launch_bounds__(kBlock) void hits_kernel(SceneView S, const double*
 // host launch plumbing
 
 static dev::SceneView view_of(const DeviceCopy& c) {
-    return dev::SceneView{c.nodes, c.fnodes, 0, c.refs, c.spheres, c.spair, 0, c.sphere_mat, c.quads, c.quad_mat,
-                          c.mats, c.quadf, c.sphere_mrec, c.quad_mrec, 0, c.quadbox};
+    dev::SceneView v{c.nodes, c.fnodes, 0, c.refs, c.spheres, c.spair, 0, c.sphere_mat, c.quads, c.quad_mat,
+                     c.mats, c.quadf, c.sphere_mrec, c.quad_mrec, 0, c.quadbox};
+    v.guard = c.guard;
+    return v;
 }
 
 int device_count(int* n) {
@@ -2048,8 +2045,6 @@ int device_upload(crt_scene* s, int device) {
             f.w1 = kLeafFlagF | n.count;
         }
     }
-    size_t off_nodes = 0;
-    size_t off_fnodes = align256(off_nodes + n_nodes * sizeof(DevNode));
     // sphere pair records of the f32 candidate filter (slots i, i + 1)
     std::vector<DevSpherePair> spair(n_sp);
     bool spheres_f32_ok = true;
@@ -2082,18 +2077,13 @@ int device_upload(crt_scene* s, int device) {
         if (!quad_record(q.v, q.s1, q.s2, q.sn, quadf[i])) quads_f32_ok = false;
         if (!quad_flat_box(q.v, q.s1, q.s2, quadbox[i])) quads_flat_ok = false;
     }
-    size_t off_refs = align256(off_fnodes + n_nodes * sizeof(DevNodeF));
-    size_t off_sp = align256(off_refs + n_refs * 4);
-    size_t off_spp = align256(off_sp + n_sp * sizeof(DevSphere));
-    size_t off_spm = align256(off_spp + n_sp * sizeof(DevSpherePair));
-    size_t off_q = align256(off_spm + n_sp * 4);
-    size_t off_qf = align256(off_q + n_q * sizeof(DevQuad));
-    size_t off_qb = align256(off_qf + n_q * sizeof(DevQuadF));
-    size_t off_qm = align256(off_qb + n_q * sizeof(DevQuadBox));
-    size_t off_m = align256(off_qm + n_q * 4);
-    size_t off_smr = align256(off_m + std::max<size_t>(1, n_m) * sizeof(DevMaterial));
-    size_t off_qmr = align256(off_smr + n_sp * sizeof(DevMaterial));
-    size_t total = align256(off_qmr + n_q * sizeof(DevMaterial));
+    size_t off[kArrCount + 1];
+    const size_t total = device_layout(s, off);
+    const size_t off_nodes = off[kArrNodes], off_fnodes = off[kArrFNodes], off_refs = off[kArrRefs];
+    const size_t off_sp = off[kArrSpheres], off_spp = off[kArrSpherePairs], off_spm = off[kArrSphereMat];
+    const size_t off_q = off[kArrQuads], off_qf = off[kArrQuadF], off_qb = off[kArrQuadBox];
+    const size_t off_qm = off[kArrQuadMat], off_m = off[kArrMats], off_smr = off[kArrSphereMrec];
+    const size_t off_qmr = off[kArrQuadMrec], off_guard = off[kArrGuard];
     std::vector<DevMaterial> smrec(n_sp), qmrec(n_q);
     // Shading constants precomputed per slot, with the reference's own operations (IEEE f64, no
     // contraction), so shade reads the values its divisions would give:
@@ -2141,6 +2131,7 @@ int device_upload(crt_scene* s, int device) {
     if (e == hipSuccess) e = up(off_m, s->dmats.data(), n_m * sizeof(DevMaterial));
     if (e == hipSuccess) e = up(off_smr, smrec.data(), n_sp * sizeof(DevMaterial));
     if (e == hipSuccess) e = up(off_qmr, qmrec.data(), n_q * sizeof(DevMaterial));
+    if (e == hipSuccess) e = hipMemset(b + off_guard, 0, 64);
     if (e != hipSuccess) {
         (void)hipFree(base);
         return fail(CRT_E_HIP, std::string("scene upload: ") + hipGetErrorString(e));
@@ -2165,7 +2156,25 @@ int device_upload(crt_scene* s, int device) {
     c.mats = reinterpret_cast<DevMaterial*>(b + off_m);
     c.sphere_mrec = reinterpret_cast<DevMaterial*>(b + off_smr);
     c.quad_mrec = reinterpret_cast<DevMaterial*>(b + off_qmr);
+    c.guard = reinterpret_cast<unsigned long long*>(b + off_guard);
     c.valid = true;
+    return CRT_OK;
+}
+
+// the guard words of the scene's copy on `device` (after the renders that count into them have
+// completed: synchronizes the device)
+int device_guard(crt_scene* s, int device, uint64_t* schlick_undecided, bool reset) {
+    int rc = check_device(device);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> lk(s->mu);
+    DeviceCopy& c = s->dev[device];
+    if (!c.valid) return fail(CRT_E_NOT_UPLOADED, "crt_render_guard: scene not uploaded to this device");
+    DeviceGuard g(device);
+    HIP_TRY(hipDeviceSynchronize());
+    unsigned long long v = 0;
+    HIP_TRY(hipMemcpy(&v, c.guard, sizeof v, hipMemcpyDeviceToHost));
+    if (reset) HIP_TRY(hipMemset(c.guard, 0, sizeof v));
+    *schlick_undecided = v;
     return CRT_OK;
 }
 

@@ -1101,11 +1101,8 @@ int crt_scene_info_get(const crt_scene* s, crt_scene_info* info) {
     r.num_nodes = s->nodes.size();
     r.depth = s->depth;
     r.max_leaf_size = s->max_leaf;
-    r.device_bytes = s->dnodes.size() * sizeof(DevNode) + s->refs.size() * 4 +
-                     s->spheres.size() * sizeof(DevSphere) + s->sphere_mat.size() * 4 +
-                     s->quads.size() * sizeof(DevQuad) + s->quad_mat.size() * 4 +
-                     s->dmats.size() * sizeof(DevMaterial) +
-                     (s->spheres.size() + s->quads.size()) * sizeof(DevMaterial);  // per-slot copies
+    size_t off[kArrCount + 1];
+    r.device_bytes = device_layout(s, off);  // the allocation device_upload makes
     r.build_ms = s->build_ms;
     *info = r;
     return CRT_OK;
@@ -1201,6 +1198,12 @@ int crt_closest_hits(crt_scene* s, int device, const double* rays, size_t n, dou
     clear_error();
     if (!s || (n && (!rays || !out))) return fail(CRT_E_INVALID, "crt_closest_hits: null argument");
     return device_closest_hits(s, device, rays, n, t_min, t_max, out);
+}
+
+int crt_render_guard(crt_scene* s, int device, uint64_t* schlick_undecided, int reset) {
+    clear_error();
+    if (!s || !schlick_undecided) return fail(CRT_E_INVALID, "crt_render_guard: null argument");
+    return device_guard(s, device, schlick_undecided, reset != 0);
 }
 
 }  // extern "C"

@@ -117,6 +117,9 @@ struct DeviceCopy {
     double* partial = nullptr;
     size_t partial_bytes = 0;
     unsigned long long* counters = nullptr;   // instrumented pass
+    // parity guard words (zeroed at upload): [0] Dielectric reflect-or-refract decisions that a
+    // 1-ulp difference of pow(1 - cos, 5) could have flipped (shade(), crt_render_guard)
+    unsigned long long* guard = nullptr;
 };
 
 // A flattened primitive (Scene::get_primitive_components order) with the derived data the
@@ -154,6 +157,27 @@ struct crt_scene {
 };
 
 namespace crt {
+// The one device allocation of a scene copy (device_upload): 256-byte aligned sub-arrays in this
+// order; crt_scene_info reports its total as device_bytes.
+enum DevArray { kArrNodes, kArrFNodes, kArrRefs, kArrSpheres, kArrSpherePairs, kArrSphereMat, kArrQuads,
+                kArrQuadF, kArrQuadBox, kArrQuadMat, kArrMats, kArrSphereMrec, kArrQuadMrec, kArrGuard,
+                kArrCount };
+inline size_t device_layout(const crt_scene* s, size_t off[kArrCount + 1]) {
+    const size_t n_nodes = s->dnodes.size(), n_sp = s->spheres.size(), n_q = s->quads.size();
+    const size_t bytes[kArrCount] = {
+        n_nodes * sizeof(DevNode), n_nodes * sizeof(DevNodeF), s->refs.size() * 4, n_sp * sizeof(DevSphere),
+        n_sp * sizeof(DevSpherePair), n_sp * 4, n_q * sizeof(DevQuad), n_q * sizeof(DevQuadF),
+        n_q * sizeof(DevQuadBox), n_q * 4, std::max<size_t>(1, s->dmats.size()) * sizeof(DevMaterial),
+        n_sp * sizeof(DevMaterial), n_q * sizeof(DevMaterial), 64};
+    size_t o = 0;
+    for (int i = 0; i < kArrCount; ++i) {
+        off[i] = o;
+        o = (o + bytes[i] + 255) & ~size_t(255);
+    }
+    off[kArrCount] = o;
+    return o;
+}
+
 // error plumbing (crt_host.cpp)
 int fail(int code, const std::string& msg);
 void clear_error();
@@ -166,6 +190,7 @@ int device_render(const crt_scene* s, int device, const crt_camera* cam, const c
 int device_closest_hits(crt_scene* s, int device, const double* rays, size_t n, double t_min,
                         double t_max, crt_hit* out);
 int device_count(int* n);
+int device_guard(crt_scene* s, int device, uint64_t* schlick_undecided, bool reset);
 int device_build_bvh(crt_scene* s, uint32_t num_buckets, uint32_t max_leaf, int device,
                      const std::vector<double>& boxes, const std::vector<double>& cents);
 int device_ppm_values(int device, const double* d_rgb, size_t n, int32_t* h_values, void* stream);

@@ -245,6 +245,14 @@ int crt_ppm_values(int device, const double* d_rgb, size_t n, int32_t* h_values,
  * one "r g b\n" line per pixel, rows top to bottom. */
 int crt_ppm_write(const char* path, uint32_t w, uint32_t h, const int32_t* values);
 
+/* Parity guard of the renders of `scene` on `device` since its upload (or the last reset):
+ * *schlick_undecided = Dielectric reflect-or-refract decisions (material.h:199-210) whose branch
+ * would differ for a pow(1 - cos, 5) one ulp away from the kernel's correctly rounded value
+ * (cpp_raytracer_amd/csrc/crt_schlick.h). glibc's pow, which the reference calls, is within one
+ * ulp but not correctly rounded, so a render during which this stays 0 took every such branch as
+ * the reference does. Synchronizes the device; reset != 0 zeroes the count. */
+int crt_render_guard(crt_scene* scene, int device, uint64_t* schlick_undecided, int reset);
+
 #ifdef __cplusplus
 }
 #endif

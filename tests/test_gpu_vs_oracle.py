@@ -103,6 +103,7 @@ def test_baseline_config2_properties(crt):
         s.render_async(0, cam, b.data_ptr(), st, Tiling(16, 3, t, 0))
     torch.cuda.synchronize()
     assert torch.equal(a, b)
+    assert s.guard(0) == 0  # no Dielectric branch of the 4 frames depends on glibc's pow rounding
     an = a.cpu().numpy()
     assert np.isfinite(an).all() and an.min() >= 0 and an.max() <= 1
     want = orc.render(d, 2024, threads=16, crop=(396, 404, 596, 604))
