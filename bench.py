@@ -8,14 +8,27 @@ blocks, each rank renders its blocks, and the tiles are all-gathered over RCCL (
 frame on every rank: the total work is fixed, so scaling is "strong". The gather of frame i runs
 on a side stream while frame i + 1 renders (double-buffered frames).
 
+`python bench.py --gpus N` with N > 1 and no WORLD_SIZE in the environment launches the N ranks
+itself (torch.distributed.run, 127.0.0.1) before anything touches a GPU, and fails when fewer than
+N GPUs are visible; under a launcher (WORLD_SIZE set) it is one rank.
+
 Prints ONE JSON line on rank 0 (see the repo contract), with
-  roofline:     algorithmic bytes of the render kernel (56 B per BVH node visited,
-                36 B per sphere test, 124 B per parallelogram test, 24 B per pixel written; the
-                visit counts come from an untimed instrumented pass of the same frame) / the
-                kernel's average launch time (HIP events on the launch stream), against the HBM
-                peak 8 TB/s; traffic from profiles/ PMC data when present.
+  roofline:     the resource that binds the render kernel. The scene is LDS/L2-resident and the
+                kernel moves ~7 GB per launch to/from HBM (~1% of peak), so the bound is VALU
+                issue: bound "valu", frac = VALU issue cycles / SIMD cycles of the timed kernel
+                from the rocprofv3 PMC pass of this exact build (profiles/pmc_latest.json:
+                2 cycles per wave64 VALU instruction, 4 for f64 — the issue model, pinned by the
+                tools/valu_rate.hip microbenchmark), lane_util = active lanes per VALU
+                instruction. The HBM figures are reported beside it, labelled: `hbm.algorithmic`
+                = SURVEY 8d bytes (56 B per BVH node visited, 36 B per sphere test, 124 B per
+                parallelogram test, 24 B per pixel written; visit counts from an untimed
+                instrumented pass) / kernel time — bytes the path touches, almost all served by
+                LDS and L1/L2, so its "fraction" may exceed 1 — and `hbm.measured` = PMC HBM bytes
+                (FETCH_SIZE x2 + WRITE_SIZE) / kernel time against the 8 TB/s peak.
   cpu_baseline: the reference's own Camera::render (oracle/_ref, built from the reference
-                sources) timed on this host's cores over a bounded sample of the same scene.
+                sources) on the host, median of 3 runs of a bounded sample of the same frame
+                (fewer spp), threads = the CPUs this process may use (OMP_NUM_THREADS when set:
+                the GPU box's share for one GPU), CPU model and host CPU count reported.
 """
 from __future__ import annotations
 
@@ -42,13 +55,49 @@ SCENE_DATA = {
 
 
 def kernel_source_sha() -> str:
-    """Hash of the kernel sources: a PMC summary (profiles/pmc_latest.json) is used for
-    roofline.traffic only when it was collected on this exact kernel."""
+    """Hash of the kernel sources and of the library's compile-time switches (crt_build_info): a
+    PMC summary (profiles/pmc_latest.json) is used only when it was collected on this exact
+    build."""
     import hashlib
+    import cpp_raytracer_amd as crt
     h = hashlib.sha256()
-    for f in ("crt_device.hip", "crt_internal.h", "crt_quad_filter.h"):
+    for f in ("crt_device.hip", "crt_internal.h", "crt_quad_filter.h", "crt_schlick.h"):
         h.update((ROOT / "cpp_raytracer_amd" / "csrc" / f).read_bytes())
+    h.update(crt.lib().crt_build_info())
     return h.hexdigest()[:16]
+
+
+def cpu_info() -> tuple[str, int, int]:
+    """(CPU model, host CPUs, CPUs this process may use)."""
+    model = "unknown"
+    try:
+        for line in Path("/proc/cpuinfo").read_text().splitlines():
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    usable = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    return model, os.cpu_count() or 1, usable
+
+
+def self_launch(args) -> int:
+    """Run this script as N ranks (one per GPU) under torch.distributed.run and return its exit
+    code. Called before any GPU initialisation (torch.cuda.device_count() does not initialise
+    HIP on this image)."""
+    import socket
+    import torch
+    if not args.launch_check:
+        visible = torch.cuda.device_count()
+        if visible < args.gpus:
+            print(f"[bench] --gpus {args.gpus} but only {visible} GPU(s) visible", file=sys.stderr, flush=True)
+            return 2
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", str(Path(__file__).resolve()), *sys.argv[1:]]
+    return subprocess.run(cmd).returncode
 
 
 def parse():
@@ -63,8 +112,11 @@ def parse():
     ap.add_argument("--spp", type=int, default=500)
     ap.add_argument("--depth", type=int, default=50)
     ap.add_argument("--base-seed", type=int, default=2024)
-    ap.add_argument("--cpu-spp", type=int, default=500, help="spp of the CPU-baseline sample (500 = the full frame)")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, host cores)")
+    ap.add_argument("--cpu-spp", type=int, default=250, help="spp of the CPU-baseline sample (the same frame)")
+    ap.add_argument("--cpu-runs", type=int, default=3, help="CPU-baseline runs (the median is reported)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = OMP_NUM_THREADS, else the usable CPUs")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="ranks only join the process group and report (tests the N-rank launch on CPU)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pmc-json", default=str(ROOT / "profiles" / "pmc_latest.json"))
     return ap.parse_args()
@@ -72,11 +124,16 @@ def parse():
 
 def cpu_baseline(args, scene_data, log) -> dict | None:
     """Reference Camera::render on the host, on a bounded sample of the same workload."""
+    import statistics
     import cpp_raytracer_amd as crt
     from cpp_raytracer_amd import camera_with
-    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+    model, host_cpus, usable = cpu_info()
+    threads = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or usable
     ref = ROOT / "oracle" / "_ref" / "ref_driver"
-    sample = f"{args.scene} seed {args.seed}, {args.width}x{args.height}, {args.cpu_spp} spp, depth {args.depth}"
+    runs = max(1, args.cpu_runs)
+    sample = (f"{args.scene} seed {args.seed}, {args.width}x{args.height}, {args.cpu_spp} spp, depth {args.depth}; "
+              f"median of {runs} runs")
+    host = {"cpu_model": model, "host_cpus": host_cpus, "usable_cpus": usable}
     d = crt.SceneData(scene_data.materials, scene_data.objects,
                       camera_with(scene_data.camera, image_w=args.width, image_h=args.height,
                                   samples_per_pixel=args.cpu_spp, max_depth=args.depth))
@@ -85,27 +142,53 @@ def cpu_baseline(args, scene_data, log) -> dict | None:
         d.save(p)
         if ref.exists():
             try:
-                r = subprocess.run([str(ref), "time", str(p), str(threads)], capture_output=True, text=True,
-                                   timeout=600, check=True)
-                j = json.loads(r.stdout.strip().splitlines()[-1])
-                return {"value": round(j["samples"] / j["seconds"] / 1e6, 4), "unit": "Msamples/s",
-                        "cores": threads, "kind": "reference",
+                rates = []
+                for _ in range(runs):
+                    r = subprocess.run([str(ref), "time", str(p), str(threads)], capture_output=True, text=True,
+                                       timeout=600, check=True)
+                    j = json.loads(r.stdout.strip().splitlines()[-1])
+                    rates.append(j["samples"] / j["seconds"] / 1e6)
+                return {"value": round(statistics.median(rates), 4), "unit": "Msamples/s", "cores": threads,
+                        "kind": "reference", "runs": [round(x, 4) for x in rates], **host,
                         "sample": sample + " (reference Camera::render, OpenMP, own per-thread RNG)"}
             except Exception as e:  # pragma: no cover - reported, not fatal
                 log(f"reference CPU baseline failed: {e}")
         try:
             sys.path.insert(0, str(ROOT / "oracle"))
             import crt_oracle_py as orc
-            secs, n = orc.time_render(d, threads, args.base_seed)
-            return {"value": round(n / secs / 1e6, 4), "unit": "Msamples/s", "cores": threads, "kind": "port",
+            rates = []
+            for _ in range(runs):
+                secs, n = orc.time_render(d, threads, args.base_seed)
+                rates.append(n / secs / 1e6)
+            return {"value": round(statistics.median(rates), 4), "unit": "Msamples/s", "cores": threads,
+                    "kind": "port", "runs": [round(x, 4) for x in rates], **host,
                     "sample": sample + " (oracle C restatement, OpenMP)"}
         except Exception as e:  # pragma: no cover
             log(f"port CPU baseline failed: {e}")
     return None
 
 
-def main():
+def launch_check(args) -> int:
+    """One rank of `--launch-check`: join the process group (gloo, CPU), agree on the world size
+    with an all-reduce, rank 0 prints it."""
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo")
+    t = torch.ones(1)
+    dist.all_reduce(t)
+    if dist.get_rank() == 0:
+        print(json.dumps({"launch_check": True, "world_size": dist.get_world_size(), "all_reduce": float(t[0]),
+                          "requested": args.gpus}), flush=True)
+    dist.destroy_process_group()
+    return 0
+
+
+def main() -> int:
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return self_launch(args)
+    if args.launch_check:
+        return launch_check(args)
     import torch
     import torch.distributed as dist
     import cpp_raytracer_amd as crt
@@ -116,7 +199,8 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        args.gpus = world if world > 1 else args.gpus
+        print(f"[bench] --gpus {args.gpus} but WORLD_SIZE={world}: reporting the {world} ranks that run",
+              file=sys.stderr, flush=True)
     distributed = world > 1
     # one GPU per rank; CRT_BENCH_BACKEND=gloo + ranks sharing a device rehearses the N>1 path
     # on a one-GPU box (RCCL refuses two ranks on one device)
@@ -128,6 +212,8 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
+        if dist.get_world_size() != world:
+            raise SystemExit(f"process group has {dist.get_world_size()} ranks, WORLD_SIZE={world}")
 
     def log(msg):
         if rank == 0:
@@ -210,23 +296,47 @@ def main():
     workload = f"{args.scene} seed {args.seed}, {w}x{h}, {args.spp} spp, max_depth {args.depth}"
     if (args.scene, w, h, args.spp, args.depth) == ("rtow_final", 1200, 800, 500, 50):
         workload += " (BASELINE config 2)"
-    # HBM bytes per launch from the rocprofv3 PMC passes (FETCH_SIZE x2 + WRITE_SIZE, the guide's
-    # gfx950 correction; tools/gpu_pmc.sh + tools/pmc_summary.py) of this workload on this kernel
-    traffic, traffic_src, valu = None, None, None
+    # counters of the timed kernel from the rocprofv3 PMC passes (tools/gpu_pmc.sh +
+    # tools/pmc_summary.py) of this workload on this exact build
+    pmc_data, pmc_src = None, None
     pmc = Path(args.pmc_json)
     if pmc.exists() and world == 1:
         try:
             pj = json.loads(pmc.read_text())
             if pj.get("workload") == workload and pj.get("kernel_source_sha") == kernel_source_sha():
-                traffic = pj.get("hbm_bytes_per_launch")
-                traffic_src = str(pmc.relative_to(ROOT)) if pmc.is_relative_to(ROOT) else str(pmc)
-                if "valu_issue_frac" in pj:
-                    # what actually binds: VALU issue (2 SIMD32 cycles per wave64 instruction, 4 for
-                    # f64) over the chip's SIMD-cycles, and the share of lanes active per instruction
-                    valu = {"issue_frac": round(pj["valu_issue_frac"], 4),
-                            "lane_util": round(pj.get("valu_lane_utilization", 0.0), 4)}
+                pmc_data = pj
+                pmc_src = str(pmc.relative_to(ROOT)) if pmc.is_relative_to(ROOT) else str(pmc)
         except Exception:
-            traffic = None
+            pmc_data = None
+    traffic = pmc_data.get("hbm_bytes_per_launch") if pmc_data else None
+    measured_gbs = traffic / (kernel_ms * 1e-3) / 1e9 if traffic else None
+    issue = pmc_data.get("valu_issue_frac") if pmc_data else None
+    roofline = {
+        "bound": "valu",
+        "achieved": round(issue, 4) if issue is not None else None,
+        "peak": 1.0,
+        "unit": "VALU issue cycles per SIMD cycle",
+        "frac": round(issue, 4) if issue is not None else None,
+        "traffic": traffic,
+        "lane_util": round(pmc_data["valu_lane_utilization"], 4) if pmc_data and "valu_lane_utilization" in pmc_data else None,
+        "valu_model": "2 SIMD cycles per wave64 VALU instruction, 4 per f64 one, over 32 x SQ_BUSY_CYCLES "
+                      "(1024 SIMDs); tools/valu_rate.hip measures the per-instruction costs",
+        "pmc_source": pmc_src,
+        "kernel_ms": round(kernel_ms, 3),
+        "hbm": {
+            "peak_GBps": HBM_PEAK_GBS,
+            "algorithmic": {"GBps": round(achieved_gbs, 1), "frac_of_peak": round(achieved_gbs / HBM_PEAK_GBS, 4),
+                            "bytes_per_launch": int(alg_bytes),
+                            "basis": "SURVEY 8d bytes the path touches (56 B/node, 36 B/sphere test, 124 B/quad "
+                                     "test, 24 B/pixel); served almost entirely by LDS and L1/L2, not HBM"},
+            "measured": {"GBps": round(measured_gbs, 1) if measured_gbs else None,
+                         "frac_of_peak": round(measured_gbs / HBM_PEAK_GBS, 4) if measured_gbs else None,
+                         "bytes_per_launch": traffic,
+                         "basis": "rocprofv3 PMC: 2 x FETCH_SIZE + WRITE_SIZE (MI355X_MICROARCH.md HBM section)"},
+        },
+    }
+    if pmc_data is None:
+        roofline["note"] = "no PMC summary of this workload on this exact build: issue fraction and traffic unmeasured"
 
     if distributed:
         t = torch.tensor([alg_bytes, cnt.rays, cnt.samples, cnt.nodes_visited], dtype=torch.float64, device="cuda")
@@ -249,14 +359,11 @@ def main():
             "config": {"workload": workload,
                        "samples_per_step": h * w * args.spp, "primitives": int(info.num_primitives),
                        "bvh_nodes": int(info.num_nodes), "partition": f"{rb}-row blocks over {world} ranks, "
-                       "RCCL all-gather of tiles overlapped with the next frame" if distributed else "whole frame on one GPU"},
-            "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved_gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "traffic_source": traffic_src, "valu": valu,
-                         "kernel_ms": round(kernel_ms, 3),
-                         "alg_bytes_per_launch": int(alg_bytes),
-                         "basis": "SURVEY 8d algorithmic bytes (56 B/node, 36 B/sphere test, 124 B/quad test, "
-                                  "24 B/pixel); scene is LDS/L1/L2-resident, so these bytes mostly never reach HBM"},
+                       "RCCL all-gather of tiles overlapped with the next frame" if distributed else "whole frame on one GPU",
+                       "process_group": {"backend": dist.get_backend() if distributed else None,
+                                         "world_size": dist.get_world_size() if distributed else 1,
+                                         "visible_gpus": torch.cuda.device_count()}},
+            "roofline": roofline,
             "fp64": {"achieved_tflops": round(flops / (kernel_ms * 1e-3) / 1e12, 3),
                      "peak_tflops": FP64_VECTOR_PEAK_TFLOPS, "rays_per_sample": round(rays_per_sample, 4),
                      "nodes_per_ray": round(cnt.nodes_visited / max(1, cnt.rays), 3),
@@ -280,7 +387,8 @@ def main():
         print(json.dumps(out), flush=True)
     if distributed:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

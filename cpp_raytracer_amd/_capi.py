@@ -103,6 +103,7 @@ P = C.POINTER
 EXPORTS = {
     "crt_abi_version": (C.c_int, []),
     "crt_last_error": (C.c_char_p, []),
+    "crt_build_info": (C.c_char_p, []),
     "crt_device_count": (C.c_int, [P(C.c_int)]),
     "crt_free": (None, [C.c_void_p]),
     "crt_sample_seed": (C.c_uint32, [C.c_uint32, C.c_uint32, C.c_uint32]),

@@ -264,19 +264,12 @@ __device__ __forceinline__ double recip_exact(double s) {
 template <bool FAST = false>
 __device__ __forceinline__ void random_unit_vector(uint32_t& s, double& x, double& y, double& z) {
     double m2;
-#if CRT_ABLATE_RUV  // timing experiment only (wrong results): one candidate, no rejection loop
-    x = rnd_pm1(s);
-    y = rnd_pm1(s);
-    z = rnd_pm1(s);
-    m2 = x * x + y * y + z * z;
-#else
     do {
         x = rnd_pm1(s);
         y = rnd_pm1(s);
         z = rnd_pm1(s);
         m2 = x * x + y * y + z * z;
     } while (!(m2 < 1));
-#endif
     double inv = recip_exact<FAST>(sqrt_exact<FAST>(x * x + y * y + z * z));
     x = x * inv;
     y = y * inv;
@@ -1361,15 +1354,10 @@ __device__ __forceinline__ void start_path(const CamView& C, uint32_t row, uint3
         P.o[0] = C.o[0]; P.o[1] = C.o[1]; P.o[2] = C.o[2];
     } else {  // random_point_in_defocus_disk (camera.h:160-168, vec3d.h:79-85)
         double vx, vy;
-#if CRT_ABLATE_DISK  // timing experiment only (wrong results): one candidate
-        vx = rnd_pm1(rng);
-        vy = rnd_pm1(rng);
-#else
         do {
             vx = rnd_pm1(rng);
             vy = rnd_pm1(rng);
         } while (!(vx * vx + vy * vy + 0.0 * 0.0 < 1));
-#endif
         P.o[0] = (C.o[0] + C.ddx[0] * vx) + C.ddy[0] * vy;
         P.o[1] = (C.o[1] + C.ddx[1] * vx) + C.ddy[1] * vy;
         P.o[2] = (C.o[2] + C.ddx[2] * vx) + C.ddy[2] * vy;
@@ -1411,11 +1399,7 @@ __device__ __forceinline__ bool shade(const SceneView& S, const CamView& C, Path
     bool front;
     (void)hit_record<LS, true, SPH, QONLY>(S, ref, P.o, P.d, t, p, n, front, M.emit[0]);
     const uint32_t kind = M.kind;
-#if CRT_ABLATE_MAT  // timing experiment only (wrong results): every scattering material as Lambertian
-    const bool lam = kind == CRT_LAMBERTIAN || kind == CRT_METAL || kind == CRT_DIELECTRIC, met = false, die = false;
-#else
     const bool lam = kind == CRT_LAMBERTIAN, met = kind == CRT_METAL, die = kind == CRT_DIELECTRIC;
-#endif
     if (!(lam || met || die)) {  // DiffuseLight: emits, never scatters (material.h:248-263)
         acc[0] = acc[0] + P.T[0] * M.emit[0];
         acc[1] = acc[1] + P.T[1] * M.emit[1];
@@ -2695,6 +2679,22 @@ int render_multi(crt_scene* s, const crt_camera* cam, int num_devices, double* h
         stats->kernel_ms = max_ms;
     }
     return rc;
+}
+
+// The compile-time switches this library was built with (bench.py hashes them with the kernel
+// sources, so a PMC summary is only used for the exact build it was collected on).
+#define CRT_STR2(x) #x
+#define CRT_STR(x) CRT_STR2(x)
+const char* device_build_info() {
+    return "arch=gfx950 CRT_BLOCK=" CRT_STR(CRT_BLOCK) " CRT_TILE_W=" CRT_STR(CRT_TILE_W)
+           " CRT_SPEC_MASKED=" CRT_STR(CRT_SPEC_MASKED) " CRT_ACC_LDS=" CRT_STR(CRT_ACC_LDS)
+           " CRT_MANY_WAVES=" CRT_STR(CRT_MANY_WAVES) " CRT_EXACT_SHORTCUTS=" CRT_STR(CRT_EXACT_SHORTCUTS)
+           " CRT_WAVES_PER_EU=" CRT_STR(CRT_WAVES_PER_EU) " CRT_WAVES_PER_EU_LDS=" CRT_STR(CRT_WAVES_PER_EU_LDS)
+           " CRT_SHADE_BATCH=" CRT_STR(CRT_SHADE_BATCH) " CRT_SHADE_MIN=" CRT_STR(CRT_SHADE_MIN)
+           " CRT_PENDING_MAX=" CRT_STR(CRT_PENDING_MAX) " CRT_TOP_TREELET=" CRT_STR(CRT_TOP_TREELET)
+           " CRT_SPEC_WALK=" CRT_STR(CRT_SPEC_WALK) " CRT_COUNT_SPEC=" CRT_STR(CRT_COUNT_SPEC)
+           " CRT_PRIO_WALK=" CRT_STR(CRT_PRIO_WALK) " CRT_PRIO_LEAF=" CRT_STR(CRT_PRIO_LEAF)
+           " CRT_PRIO_SHADE=" CRT_STR(CRT_PRIO_SHADE) " CRT_CHUNK_MIN=" CRT_STR(CRT_CHUNK_MIN);
 }
 
 }  // namespace crt

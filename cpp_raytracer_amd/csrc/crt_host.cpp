@@ -1015,6 +1015,8 @@ int crt_abi_version(void) { return CRT_ABI_VERSION; }
 
 const char* crt_last_error(void) { return g_last_error.c_str(); }
 
+const char* crt_build_info(void) { return device_build_info(); }
+
 void crt_free(void* p) { std::free(p); }
 
 uint32_t crt_sample_seed(uint32_t base_seed, uint32_t pixel, uint32_t sample) {

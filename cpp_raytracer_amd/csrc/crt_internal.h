@@ -190,6 +190,7 @@ int device_render(const crt_scene* s, int device, const crt_camera* cam, const c
 int device_closest_hits(crt_scene* s, int device, const double* rays, size_t n, double t_min,
                         double t_max, crt_hit* out);
 int device_count(int* n);
+const char* device_build_info();
 int device_guard(crt_scene* s, int device, uint64_t* schlick_undecided, bool reset);
 int device_build_bvh(crt_scene* s, uint32_t num_buckets, uint32_t max_leaf, int device,
                      const std::vector<double>& boxes, const std::vector<double>& cents);

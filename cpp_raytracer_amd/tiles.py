@@ -38,7 +38,6 @@ class TileGather:
         self.dst = torch.tensor(dst, dtype=torch.long, device=device)
         self.src = torch.tensor(src, dtype=torch.long, device=device)
         self.tile = torch.zeros(self.max_rows, width, 3, dtype=dtype, device=device)
-        self.parts = [torch.zeros_like(self.tile) for _ in range(world)]
         self.full = torch.zeros(world * self.max_rows, width, 3, dtype=dtype, device=device)
 
     def gather(self, frame: torch.Tensor) -> torch.Tensor:
@@ -47,8 +46,8 @@ class TileGather:
         if self.world == 1:
             return frame
         self.tile[: self.n_mine].copy_(frame.index_select(0, self.mine))
-        dist.all_gather(self.parts, self.tile, group=self.group)
-        torch.cat(self.parts, out=self.full)
+        # one all-gather straight into the rank-major tile array (no per-rank parts + concat)
+        dist.all_gather_into_tensor(self.full, self.tile, group=self.group)
         out = torch.empty_like(frame)
         out.index_copy_(0, self.dst, self.full.index_select(0, self.src))
         return out

@@ -178,6 +178,9 @@ typedef struct crt_render_stats {
 /* ---- entry points ---------------------------------------------------------------------- */
 int crt_abi_version(void);
 const char* crt_last_error(void);
+/* The library's compile-time configuration ("arch=gfx950 CRT_BLOCK=256 ..."): the kernel build
+ * switches documented in INTEGRATION.md. */
+const char* crt_build_info(void);
 int crt_device_count(int* count);
 void crt_free(void* p);
 

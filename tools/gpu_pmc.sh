@@ -1,15 +1,29 @@
 #!/bin/bash
-# Counter collection: one rocprofv3 pass per counter group (no --pmc mixed with tracing options).
+# PMC passes of one bench workload: one rocprofv3 --pmc run per counter group (no --pmc mixed with
+# tracing options; at most 8 SQ / 4 TCC / 2 GRBM per pass), each under its own time limit, then
+# tools/pmc_summary.py -> <outdir>/summary.json.
+#   tools/gpu_pmc.sh <outdir under gpurun_out> [bench.py args]
+# Counters absent from `rocprofv3 -L` on this box are dropped from their pass.
 set -o pipefail
-mkdir -p gpurun_out/pmc
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$R/$1
+shift
+ARGS="--steps 1 --warmup 0 --no-cpu-baseline $*"
+mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd /tmp
-R=$GRAFT_REPO_ROOT
-ARGS=${PMC_BENCH_ARGS:---steps 1 --warmup 0 --no-cpu-baseline}
-timeout -k 10 120 rocprofv3 -L > $R/gpurun_out/pmc/counters_list.txt 2>&1
+[ -s "$R/gpurun_out/counters_list.txt" ] || timeout -k 10 120 rocprofv3 -L > "$R/gpurun_out/counters_list.txt" 2>&1
+have() { grep -qw "$1" "$R/gpurun_out/counters_list.txt"; }
+pick() { local out=""; for c in "$@"; do have "${c%_sum}" && out="$out $c"; done; echo $out; }
+P1=$(pick FETCH_SIZE GRBM_GUI_ACTIVE)
+P2=$(pick WRITE_SIZE TCC_HIT_sum TCC_MISS_sum)
+P3=$(pick SQ_INSTS_VALU SQ_BUSY_CYCLES SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU)
+P4=$(pick SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVES SQ_LDS_BANK_CONFLICT)
 i=0
-for grp in "$@"; do
+for grp in "$P1" "$P2" "$P3" "$P4"; do
   i=$((i+1))
-  timeout -k 10 600 rocprofv3 --pmc $grp --kernel-trace --output-format csv -d $R/gpurun_out/pmc/p$i -o run -- python3 $R/bench.py $ARGS > $R/gpurun_out/pmc/bench_p$i.json 2> $R/gpurun_out/pmc/bench_p$i.err || { echo "pmc pass $i ($grp) failed"; tail -5 $R/gpurun_out/pmc/bench_p$i.err; exit 1; }
-  echo "pass $i ok: $grp"
+  [ -n "$grp" ] || continue
+  timeout -s KILL 240 rocprofv3 --pmc $grp --kernel-trace --output-format csv -d "$OUT/p$i" -o run -- python3 "$R/bench.py" $ARGS > "$OUT/bench_p$i.json" 2> "$OUT/bench_p$i.err" || { echo "pmc pass $i ($grp) failed"; tail -5 "$OUT/bench_p$i.err"; exit 1; }
+  echo "pmc pass $i ok: $grp"
 done
+cd "$R" && python tools/pmc_summary.py "$OUT" "$OUT/summary.json" > /dev/null && echo "pmc summary ok: $OUT/summary.json"
