@@ -17,6 +17,7 @@
 #include <cstring>
 #include <limits>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "crt_internal.h"
@@ -1987,20 +1988,12 @@ struct DeviceGuard {
 
 static size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
-int device_upload(crt_scene* s, int device) {
-    int rc = check_device(device);
-    if (rc) return rc;
-    std::lock_guard<std::mutex> lk(s->mu);
-    DeviceCopy& c = s->dev[device];
-    if (c.valid) return CRT_OK;
-    DeviceGuard g(device);
-    // one allocation, sub-arrays 256-byte aligned; slot refs stored twice: refs, then the
-    // ref -> primitive map the hit queries report with.
+// The device image of a scene: every array of device_layout() at its offset in one host buffer,
+// built once per scene (the first upload) and copied whole to each device.
+static void stage_image(crt_scene* s) {
     const size_t n_nodes = s->dnodes.size(), n_refs = s->refs.size();
     const size_t n_sp = s->spheres.size(), n_q = s->quads.size(), n_m = s->dmats.size();
     // f32 refs are byte offsets (index << 5) and interior w1 must stay below kLeafFlagF
-    if (n_nodes >= (size_t{1} << (31 - kNodeFShift)))
-        return fail(CRT_E_INVALID, "BVH too large for the device node layout");
     std::vector<DevNodeF> fnodes(n_nodes);
     bool f32_ok = true;
     for (size_t i = 0; i < n_nodes; ++i) {
@@ -2094,53 +2087,79 @@ int device_upload(crt_scene* s, int device) {
         qmrec[i] = s->dmats[s->quad_mat[i]];
         shading_consts(qmrec[i], nullptr);
     }
+    std::vector<char>& img = s->image;
+    img.assign(total, 0);  // the guard words upload as zeros
+    auto put = [&](size_t off, const void* src, size_t bytes) {
+        if (bytes) std::memcpy(img.data() + off, src, bytes);
+    };
+    put(off_nodes, s->dnodes.data(), n_nodes * sizeof(DevNode));
+    put(off_fnodes, fnodes.data(), n_nodes * sizeof(DevNodeF));
+    put(off_refs, s->refs.data(), n_refs * 4);
+    put(off_sp, s->spheres.data(), n_sp * sizeof(DevSphere));
+    put(off_spp, spair.data(), n_sp * sizeof(DevSpherePair));
+    put(off_spm, s->sphere_mat.data(), n_sp * 4);
+    put(off_q, s->quads.data(), n_q * sizeof(DevQuad));
+    put(off_qf, quadf.data(), n_q * sizeof(DevQuadF));
+    put(off_qb, quadbox.data(), n_q * sizeof(DevQuadBox));
+    put(off_qm, s->quad_mat.data(), n_q * 4);
+    put(off_m, s->dmats.data(), n_m * sizeof(DevMaterial));
+    put(off_smr, smrec.data(), n_sp * sizeof(DevMaterial));
+    put(off_qmr, qmrec.data(), n_q * sizeof(DevMaterial));
+    (void)off_guard;
+    s->image_f32_ok = f32_ok;
+    s->image_spheres_f32_ok = spheres_f32_ok;
+    s->image_quads_f32_ok = quads_f32_ok;
+    s->image_quads_flat_ok = quads_flat_ok;
+    s->staged = true;
+}
+
+// Copy the scene into HBM of `device`: the staged image in one transfer. Uploads to different
+// devices run concurrently (render_multi uploads from one thread per device); the image is
+// staged once, under the scene's lock.
+int device_upload(crt_scene* s, int device) {
+    int rc = check_device(device);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> lk(s->dev_mu[device]);
+    DeviceCopy& c = s->dev[device];
+    if (c.valid) return CRT_OK;
+    if (s->dnodes.size() >= (size_t{1} << (31 - kNodeFShift)))
+        return fail(CRT_E_INVALID, "BVH too large for the device node layout");
+    {
+        std::lock_guard<std::mutex> ls(s->mu);
+        if (!s->staged) stage_image(s);
+    }
+    size_t off[kArrCount + 1];
+    const size_t total = device_layout(s, off);
+    DeviceGuard g(device);
     void* base = nullptr;
     HIP_TRY(hipMalloc(&base, total));
     char* b = static_cast<char*>(base);
-    auto up = [&](size_t off, const void* src, size_t bytes) -> hipError_t {
-        if (!bytes) return hipSuccess;
-        return hipMemcpy(b + off, src, bytes, hipMemcpyHostToDevice);
-    };
-    hipError_t e = hipSuccess;
-    if (e == hipSuccess) e = up(off_nodes, s->dnodes.data(), n_nodes * sizeof(DevNode));
-    if (e == hipSuccess) e = up(off_fnodes, fnodes.data(), n_nodes * sizeof(DevNodeF));
-    if (e == hipSuccess) e = up(off_refs, s->refs.data(), n_refs * 4);
-    if (e == hipSuccess) e = up(off_sp, s->spheres.data(), n_sp * sizeof(DevSphere));
-    if (e == hipSuccess) e = up(off_spp, spair.data(), n_sp * sizeof(DevSpherePair));
-    if (e == hipSuccess) e = up(off_spm, s->sphere_mat.data(), n_sp * 4);
-    if (e == hipSuccess) e = up(off_q, s->quads.data(), n_q * sizeof(DevQuad));
-    if (e == hipSuccess) e = up(off_qf, quadf.data(), n_q * sizeof(DevQuadF));
-    if (e == hipSuccess) e = up(off_qb, quadbox.data(), n_q * sizeof(DevQuadBox));
-    if (e == hipSuccess) e = up(off_qm, s->quad_mat.data(), n_q * 4);
-    if (e == hipSuccess) e = up(off_m, s->dmats.data(), n_m * sizeof(DevMaterial));
-    if (e == hipSuccess) e = up(off_smr, smrec.data(), n_sp * sizeof(DevMaterial));
-    if (e == hipSuccess) e = up(off_qmr, qmrec.data(), n_q * sizeof(DevMaterial));
-    if (e == hipSuccess) e = hipMemset(b + off_guard, 0, 64);
+    hipError_t e = hipMemcpy(b, s->image.data(), total, hipMemcpyHostToDevice);
     if (e != hipSuccess) {
         (void)hipFree(base);
         return fail(CRT_E_HIP, std::string("scene upload: ") + hipGetErrorString(e));
     }
     c.base = base;
     c.bytes = total;
-    c.nodes = reinterpret_cast<DevNode*>(b + off_nodes);
-    c.fnodes = reinterpret_cast<DevNodeF*>(b + off_fnodes);
-    c.f32_ok = f32_ok && std::getenv("CRT_F64_NODES") == nullptr;
-    c.refs = reinterpret_cast<uint32_t*>(b + off_refs);
-    c.spheres = reinterpret_cast<DevSphere*>(b + off_sp);
-    c.spair = reinterpret_cast<DevSpherePair*>(b + off_spp);
-    c.spheres_f32_ok = spheres_f32_ok && std::getenv("CRT_F64_SPHERES") == nullptr;
-    c.sphere_mat = reinterpret_cast<uint32_t*>(b + off_spm);
-    c.quads = reinterpret_cast<DevQuad*>(b + off_q);
-    c.quadf = reinterpret_cast<DevQuadF*>(b + off_qf);
-    c.quads_f32_ok = quads_f32_ok && std::getenv("CRT_F64_QUADS") == nullptr;
-    c.quadbox = reinterpret_cast<DevQuadBox*>(b + off_qb);
+    c.nodes = reinterpret_cast<DevNode*>(b + off[kArrNodes]);
+    c.fnodes = reinterpret_cast<DevNodeF*>(b + off[kArrFNodes]);
+    c.f32_ok = s->image_f32_ok && std::getenv("CRT_F64_NODES") == nullptr;
+    c.refs = reinterpret_cast<uint32_t*>(b + off[kArrRefs]);
+    c.spheres = reinterpret_cast<DevSphere*>(b + off[kArrSpheres]);
+    c.spair = reinterpret_cast<DevSpherePair*>(b + off[kArrSpherePairs]);
+    c.spheres_f32_ok = s->image_spheres_f32_ok && std::getenv("CRT_F64_SPHERES") == nullptr;
+    c.sphere_mat = reinterpret_cast<uint32_t*>(b + off[kArrSphereMat]);
+    c.quads = reinterpret_cast<DevQuad*>(b + off[kArrQuads]);
+    c.quadf = reinterpret_cast<DevQuadF*>(b + off[kArrQuadF]);
+    c.quads_f32_ok = s->image_quads_f32_ok && std::getenv("CRT_F64_QUADS") == nullptr;
+    c.quadbox = reinterpret_cast<DevQuadBox*>(b + off[kArrQuadBox]);
     // CRT_GENERIC_QUADS=1: the generic parallelogram filter even for axis-aligned ones
-    c.quads_flat_ok = quads_flat_ok && std::getenv("CRT_GENERIC_QUADS") == nullptr;
-    c.quad_mat = reinterpret_cast<uint32_t*>(b + off_qm);
-    c.mats = reinterpret_cast<DevMaterial*>(b + off_m);
-    c.sphere_mrec = reinterpret_cast<DevMaterial*>(b + off_smr);
-    c.quad_mrec = reinterpret_cast<DevMaterial*>(b + off_qmr);
-    c.guard = reinterpret_cast<unsigned long long*>(b + off_guard);
+    c.quads_flat_ok = s->image_quads_flat_ok && std::getenv("CRT_GENERIC_QUADS") == nullptr;
+    c.quad_mat = reinterpret_cast<uint32_t*>(b + off[kArrQuadMat]);
+    c.mats = reinterpret_cast<DevMaterial*>(b + off[kArrMats]);
+    c.sphere_mrec = reinterpret_cast<DevMaterial*>(b + off[kArrSphereMrec]);
+    c.quad_mrec = reinterpret_cast<DevMaterial*>(b + off[kArrQuadMrec]);
+    c.guard = reinterpret_cast<unsigned long long*>(b + off[kArrGuard]);
     c.valid = true;
     return CRT_OK;
 }
@@ -2150,7 +2169,7 @@ int device_upload(crt_scene* s, int device) {
 int device_guard(crt_scene* s, int device, uint64_t* schlick_undecided, bool reset) {
     int rc = check_device(device);
     if (rc) return rc;
-    std::lock_guard<std::mutex> lk(s->mu);
+    std::lock_guard<std::mutex> lk(s->dev_mu[device]);
     DeviceCopy& c = s->dev[device];
     if (!c.valid) return fail(CRT_E_NOT_UPLOADED, "crt_render_guard: scene not uploaded to this device");
     DeviceGuard g(device);
@@ -2613,6 +2632,15 @@ int device_ppm_values(int device, const double* d_rgb, size_t n, int32_t* h_valu
     return CRT_OK;
 }
 
+// crt_render: the whole frame over devices [0, n). Rows are dealt in 4-row blocks (row r on device
+// (r / 4) % n, crt_tiling{4, n, d}); the scene is uploaded to every device concurrently (one host
+// thread per device, one copy of the staged image each); each device renders its rows into its
+// own frame buffer on its own stream; device 0's stream then waits for each device and pulls that
+// device's row blocks into its frame with ONE strided peer copy (hipMemcpy2DAsync over xGMI: the
+// blocks are 4 rows apart by n x 4 rows), and the assembled frame crosses PCIe once. Frames are
+// bit-identical for any n (per-sample RNG, spp-only sample chunks).
+// CRT_EMULATE_DEVICES=k (tests): k logical devices all on device 0, through the same tiling and
+// gather code.
 int render_multi(crt_scene* s, const crt_camera* cam, int num_devices, double* h_rgb,
                  crt_render_stats* stats) {
     int avail = 0;
@@ -2620,54 +2648,91 @@ int render_multi(crt_scene* s, const crt_camera* cam, int num_devices, double* h
         return fail(CRT_E_NODEVICE, "no HIP device visible (the render path has no CPU fallback)");
     if (num_devices <= 0) num_devices = avail;
     num_devices = std::min(num_devices, std::min(avail, kMaxDevices));
-    const size_t frame = static_cast<size_t>(cam->image_h) * cam->image_w * 3;
-    std::vector<double*> bufs(num_devices, nullptr);
-    std::vector<hipStream_t> streams(num_devices, nullptr);
-    std::vector<hipEvent_t> ev0(num_devices, nullptr), ev1(num_devices, nullptr);
+    bool emulate = false;
+    if (const char* e = std::getenv("CRT_EMULATE_DEVICES")) {
+        num_devices = std::max(1, std::min(std::atoi(e), 64));
+        emulate = true;
+    }
+    const int n = num_devices;
+    auto phys = [&](int d) { return emulate ? 0 : d; };
+    const size_t W = cam->image_w, H = cam->image_h;
+    const size_t frame = H * W * 3;
     const uint32_t rb = 4;  // 4-row blocks: 800 rows split exactly over 1, 2, 4, 8 devices
+    // 1. concurrent uploads, one thread per physical device
+    const int n_phys = emulate ? 1 : n;
+    std::vector<int> urc(n_phys, CRT_OK);
+    {
+        std::vector<std::thread> th;
+        for (int d = 0; d < n_phys; ++d) th.emplace_back([&, d] { urc[d] = device_upload(s, d); });
+        for (auto& t : th) t.join();
+    }
+    for (int d = 0; d < n_phys; ++d)
+        if (urc[d]) return urc[d];
+    // 2. render: each logical device into its own frame buffer on its own stream
+    std::vector<double*> bufs(n, nullptr);
+    std::vector<hipStream_t> streams(n, nullptr);
+    std::vector<hipEvent_t> ev0(n, nullptr), ev1(n, nullptr);
     int rc = CRT_OK;
-    for (int d = 0; d < num_devices && rc == CRT_OK; ++d) {
-        rc = device_upload(s, d);
-        if (rc) break;
-        DeviceGuard g(d);
-        if (hipStreamCreate(&streams[d]) != hipSuccess ||
+    for (int d = 0; d < n && rc == CRT_OK; ++d) {
+        DeviceGuard g(phys(d));
+        if (hipStreamCreateWithFlags(&streams[d], hipStreamNonBlocking) != hipSuccess ||
             hipMalloc(&bufs[d], frame * sizeof(double)) != hipSuccess ||
             hipEventCreate(&ev0[d]) != hipSuccess || hipEventCreate(&ev1[d]) != hipSuccess) {
-            rc = fail(CRT_E_HIP, "render: per-device setup failed on device " + std::to_string(d));
+            rc = fail(CRT_E_HIP, "render: per-device setup failed on device " + std::to_string(phys(d)));
             break;
         }
-        crt_tiling t{rb, static_cast<uint32_t>(num_devices), static_cast<uint32_t>(d), 0};
+        crt_tiling t{rb, static_cast<uint32_t>(n), static_cast<uint32_t>(d), 0};
         (void)hipEventRecord(ev0[d], streams[d]);
-        rc = device_render(s, d, cam, &t, bufs[d], streams[d], nullptr);
+        rc = device_render(s, phys(d), cam, &t, bufs[d], streams[d], nullptr);
         (void)hipEventRecord(ev1[d], streams[d]);
     }
-    float max_ms = 0;
-    for (int d = 0; d < num_devices; ++d) {
-        if (!streams[d]) continue;
-        DeviceGuard g(d);
-        hipError_t e = hipStreamSynchronize(streams[d]);
-        if (e != hipSuccess && rc == CRT_OK)
-            rc = fail(CRT_E_HIP, std::string("render on device ") + std::to_string(d) + ": " +
-                                     hipGetErrorString(e));
-        if (rc == CRT_OK) {
-            float ms = 0;
-            (void)hipEventElapsedTime(&ms, ev0[d], ev1[d]);
-            max_ms = std::max(max_ms, ms);
-            // gather the owned row blocks of device d
-            for (uint32_t r0 = static_cast<uint32_t>(d) * rb; r0 < cam->image_h;
-                 r0 += rb * static_cast<uint32_t>(num_devices)) {
-                uint32_t rows = std::min(rb, cam->image_h - r0);
-                size_t off = static_cast<size_t>(r0) * cam->image_w * 3;
-                size_t bytes = static_cast<size_t>(rows) * cam->image_w * 3 * sizeof(double);
-                if (hipMemcpy(h_rgb + off, bufs[d] + off, bytes, hipMemcpyDeviceToHost) != hipSuccess) {
-                    rc = fail(CRT_E_HIP, "render: gather failed");
-                    break;
-                }
+    // 3. gather into device 0's frame: one strided copy per device (full 4-row blocks; the frame's
+    // last block may be short and is copied on its own), then one device-to-host copy
+    if (rc == CRT_OK) {
+        DeviceGuard g(0);
+        const size_t row_bytes = W * 3 * sizeof(double);
+        for (int d = 1; d < n && rc == CRT_OK; ++d) {
+            if (!emulate) {
+                hipError_t pe = hipDeviceEnablePeerAccess(d, 0);
+                if (pe != hipSuccess && pe != hipErrorPeerAccessAlreadyEnabled) (void)hipGetLastError();
             }
+            if (hipStreamWaitEvent(streams[0], ev1[d], 0) != hipSuccess) {
+                rc = fail(CRT_E_HIP, "render: gather wait failed");
+                break;
+            }
+            const size_t first = static_cast<size_t>(d) * rb, step = static_cast<size_t>(n) * rb;
+            if (first >= H) continue;
+            const size_t blocks = (H - first + step - 1) / step;     // blocks of device d
+            const size_t last = first + (blocks - 1) * step;         // first row of its last block
+            const size_t full = last + rb <= H ? blocks : blocks - 1; // blocks with all 4 rows
+            hipError_t e = hipSuccess;
+            if (full)
+                e = hipMemcpy2DAsync(bufs[0] + first * W * 3, step * row_bytes, bufs[d] + first * W * 3,
+                                     step * row_bytes, rb * row_bytes, full, hipMemcpyDeviceToDevice, streams[0]);
+            if (e == hipSuccess && full < blocks)
+                e = hipMemcpyAsync(bufs[0] + last * W * 3, bufs[d] + last * W * 3, (H - last) * row_bytes,
+                                   hipMemcpyDeviceToDevice, streams[0]);
+            if (e != hipSuccess) rc = fail(CRT_E_HIP, std::string("render: gather from device ") +
+                                                          std::to_string(d) + ": " + hipGetErrorString(e));
+        }
+        if (rc == CRT_OK) {
+            hipError_t e = hipMemcpyAsync(h_rgb, bufs[0], frame * sizeof(double), hipMemcpyDeviceToHost, streams[0]);
+            if (e == hipSuccess) e = hipStreamSynchronize(streams[0]);
+            if (e != hipSuccess) rc = fail(CRT_E_HIP, std::string("render: ") + hipGetErrorString(e));
         }
     }
-    for (int d = 0; d < num_devices; ++d) {
-        DeviceGuard g(d);
+    float max_ms = 0;
+    for (int d = 0; d < n; ++d) {
+        if (!streams[d]) continue;
+        DeviceGuard g(phys(d));
+        hipError_t e = hipStreamSynchronize(streams[d]);
+        if (e != hipSuccess && rc == CRT_OK)
+            rc = fail(CRT_E_HIP, std::string("render on device ") + std::to_string(phys(d)) + ": " + hipGetErrorString(e));
+        float ms = 0;
+        if (rc == CRT_OK && hipEventElapsedTime(&ms, ev0[d], ev1[d]) == hipSuccess) max_ms = std::max(max_ms, ms);
+    }
+    for (int d = 0; d < n; ++d) {
+        DeviceGuard g(phys(d));
         if (bufs[d]) (void)hipFree(bufs[d]);
         if (streams[d]) (void)hipStreamDestroy(streams[d]);
         if (ev0[d]) (void)hipEventDestroy(ev0[d]);

@@ -153,7 +153,12 @@ struct crt_scene {
     bool linear = false;
     bool exact_slab = false;  // some node box is inverted / NaN on an axis: walk_step EXACT only
     crt::DeviceCopy dev[crt::kMaxDevices];
-    std::mutex mu;
+    std::mutex dev_mu[crt::kMaxDevices];  // one upload per device at a time (device_upload)
+    // the device image (device_layout arrays at their offsets), staged by the first upload
+    std::vector<char> image;
+    bool staged = false;
+    bool image_f32_ok = false, image_spheres_f32_ok = false, image_quads_f32_ok = false, image_quads_flat_ok = false;
+    std::mutex mu;  // staging
 };
 
 namespace crt {
