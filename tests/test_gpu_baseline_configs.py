@@ -77,8 +77,9 @@ def test_config3_cornell_full_size(crt):
     check_tiling(crt, s, d, base, whole, 8, range(8))
     f = whole.cpu().numpy()
     assert np.isfinite(f).all() and f.min() >= 0
-    # the light (intensity 15) is seen directly; the walls are lit
-    assert f.max() > 1 and (f.mean(axis=2) > 0).mean() > 0.99
+    # the light (intensity 15) is seen directly; the room is lit (the black background shows
+    # around the open front of the box)
+    assert f.max() == 15 and (f.mean(axis=2) > 0).mean() > 0.85
     check_windows(d, f, base, [
         (0, 8, 0, 8),             # corner
         (296, 304, 296, 304),     # centre (between the boxes)
