@@ -130,6 +130,7 @@ struct Work {
     uint32_t sentinel;      // the sentinel node's reference (byte offset into the f32 nodes)
     uint32_t lds_cam;       // LDS copy of the CamView (read where used: keeps it out of SGPRs)
     uint32_t lds_acc;       // five-wave instances: the lanes' pixel sums (3 x kBlock doubles)
+    uint32_t lds_cmp;       // candidate compaction (CRT_COMPACT_CAND): kCmpWaveBytes per wave
     uint32_t f32_ok;        // node bounds fit the f32 walk's error analysis (else f64 decides)
     uint32_t spheres_f32;   // sphere-only scene within the f32 filter's range (two-pass leaves)
     uint32_t quads_f32;     // parallelogram-only scene within its f32 filter's range (two-pass leaves)
@@ -1157,10 +1158,14 @@ __device__ __forceinline__ void walk(const SceneView& S, Stack<SE>& st, const do
 // the entered leaf's primitives in order (bvh.h:635-652), then "return" to the DFS.
 // Sphere-only scenes store spheres in slot order, so the slot indexes them directly and the next
 // sphere is loaded while the current one is tested.
-template <typename SE, bool COUNT, bool TOP, bool LS, bool FAST = false>
-__device__ __forceinline__ void leaf_step(const SceneView& S, Stack<SE>& st, const double o[3],
-                                          const double d[3], double tmin, float tmin32, bool sphere_only, bool pairs,
-                                          bool qfilter, bool qflat, Trav& R, LaneCounters& ctr) {
+// CMP (candidate compaction, CRT_COMPACT_CAND): the two-pass branches (sphere pairs, flat boxes)
+// stop after pass 1 and return the candidates (bit i = the leaf's primitive i; the lane stays in
+// kLeaf); compact_candidates() then tests every lane's candidates with the whole wave. Returns 0
+// when the leaf is done.
+template <typename SE, bool COUNT, bool TOP, bool LS, bool FAST = false, bool CMP = false>
+__device__ __forceinline__ uint32_t leaf_step(const SceneView& S, Stack<SE>& st, const double o[3],
+                                              const double d[3], double tmin, float tmin32, bool sphere_only, bool pairs,
+                                              bool qfilter, bool qflat, Trav& R, LaneCounters& ctr) {
     const uint2 range = make_uint2(R.first, R.count);  // index, count
     const uint32_t end = range.x + range.y;
     const double ia = recip_a<FAST>(R.a), lo = lim_tmin(tmin, R.a);
@@ -1189,6 +1194,10 @@ __device__ __forceinline__ void leaf_step(const SceneView& S, Stack<SE>& st, con
             cand = sphere_pair_candidates(cand, rec, L);
         }
         cand &= ~(range.y & 1u);  // an odd count's last verdict is the slot after the leaf
+        if (CMP) {  // bit nbits - 1 - i -> bit i
+            cand = __builtin_bitreverse32(cand) >> (32 - nbits);
+            if (cand) return cand;
+        }
         while (cand) {
             if (COUNT) {
                 ctr.cand++;
@@ -1231,6 +1240,7 @@ __device__ __forceinline__ void leaf_step(const SceneView& S, Stack<SE>& st, con
             const float th = __builtin_fmaf(vmax_abs(lo, hi), 0x1p-19f, R.marg);
             cand |= static_cast<uint32_t>(!(hi - lo < -th)) << i;
         }
+        if (CMP && cand) return cand;
         while (cand) {
             if (COUNT) {
                 ctr.cand++;
@@ -1327,6 +1337,121 @@ __device__ __forceinline__ void leaf_step(const SceneView& S, Stack<SE>& st, con
     }
     // the pop after the leaf was made by walk (R.cur is the next node, unless the stack was empty)
     R.state = R.sp < 0 ? kDone : kWalk;
+    return 0;
+}
+
+// Candidate compaction (the north star's ballot / prefix compaction, applied where the wave's
+// lanes are least used: pass 2 of the two-pass leaves, 25-33% lane utilization when each lane
+// tests its own 0-12 candidates). Every lane of the wave takes part: the deferred candidates of
+// all lanes (leaf_step<CMP>) become one dense list of (owner lane, primitive) items (bit-plane
+// ballots give each owner its exclusive prefix), the wave tests 64 items per iteration with the
+// owner's ray read across lanes (ds_bpermute), and each owner's closest hit is the minimum of
+// (t, primitive index) over its items (LDS atomics on t's bits, then on the index among the
+// items at that t). That equals the sequential loop: a candidate tested at the leaf-entry t_max
+// reports t iff the sequential loop's shrinking t_max would accept it at t (the sphere's first
+// root in (t_min, T) is the same for any T above it, and a parallelogram's t does not depend on
+// T), and the strict `t < t_max` update keeps the first of equal t in slot order.
+constexpr uint32_t kCmpCap = 128;  // items per wave and round (more: the per-lane loop)
+constexpr uint32_t kCmpWaveBytes = 64 * 8 + 64 * 4 + kCmpCap * 4;
+typedef __attribute__((address_space(3))) unsigned long long LdsU64;
+typedef __attribute__((address_space(3))) uint32_t LdsU32;
+
+template <bool LS, bool QUAD, bool COUNT, bool FAST>
+__device__ __forceinline__ void compact_candidates(const SceneView& S, uint32_t lds_cmp, const double o[3],
+                                                   const double d[3], double tmin, uint32_t defer, Trav& R,
+                                                   LaneCounters& ctr) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t base = lds_cmp + (threadIdx.x >> 6) * kCmpWaveBytes;
+    LdsU64* const tkey = (LdsU64*)static_cast<uintptr_t>(base);
+    LdsU32* const best = (LdsU32*)static_cast<uintptr_t>(base + 64 * 8);
+    LdsU32* const list = (LdsU32*)static_cast<uintptr_t>(base + 64 * 12);
+    // exclusive prefix of the candidate counts over the lanes (counts <= 32: six bit planes)
+    const uint32_t n = static_cast<uint32_t>(__builtin_popcount(defer));
+    uint32_t pre = 0, total = 0;
+#pragma unroll
+    for (uint32_t b = 0; b < 6; ++b) {
+        const uint64_t m = __ballot((n >> b) & 1u);
+        pre += __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32), __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0u)) << b;
+        total += static_cast<uint32_t>(__popcll(m)) << b;
+    }
+    if (COUNT) ctr.cand += n;
+    const double ia = QUAD ? 0.0 : recip_a<FAST>(R.a);
+    if (total > kCmpCap) {  // the per-lane loop of leaf_step
+        uint32_t m = defer;
+        while (m) {
+            if (COUNT && wave_leader()) ctr.it_cand++;
+            const uint32_t i = R.first + static_cast<uint32_t>(__builtin_ctz(m));
+            m &= m - 1;
+            double t;
+            bool h;
+            if constexpr (QUAD) h = hit_quad(lds_rec<DevQuad>(S.quads_lds + (i << 7)), o, d, tmin, R.tmax, t);
+            else h = hit_sphere<false>(sphere_at<LS>(S, i), o, d, R.a, ia, tmin, R.tmax, 0.0, 0.0, t);
+            if (h) {
+                R.tmax = t;
+                R.tmax32 = tmax_f32(t);
+                R.ref = (QUAD ? kRefQuad : 0u) | i;
+                R.found = true;
+            }
+        }
+        if (defer) R.state = R.sp < 0 ? kDone : kWalk;
+        return;
+    }
+    tkey[lane] = ~0ull;
+    best[lane] = ~0u;
+    for (uint32_t m = defer, k = pre; m; m &= m - 1, ++k) list[k] = lane | (static_cast<uint32_t>(__builtin_ctz(m)) << 6);
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    unsigned long long key[kCmpCap / 64];
+    uint32_t own[kCmpCap / 64], idx[kCmpCap / 64];
+#pragma unroll
+    for (uint32_t it = 0; it < kCmpCap / 64; ++it) {
+        key[it] = ~0ull;
+        own[it] = 0;
+        idx[it] = 0;
+        if (it * 64 >= total) continue;  // wave-uniform
+        if (COUNT && wave_leader()) ctr.it_cand++;
+        const uint32_t j = it * 64 + lane;
+        const bool live = j < total;
+        const uint32_t item = list[live ? j : 0];
+        own[it] = item & 63;
+        idx[it] = item >> 6;
+        const int src = static_cast<int>(own[it]);
+        const double oo[3] = {__shfl(o[0], src), __shfl(o[1], src), __shfl(o[2], src)};
+        const double dd[3] = {__shfl(d[0], src), __shfl(d[1], src), __shfl(d[2], src)};
+        const double tmax = __shfl(R.tmax, src);
+        const uint32_t i = __shfl(R.first, src) + idx[it];
+        double t = 0;
+        bool h;
+        if constexpr (QUAD) {
+            h = hit_quad(lds_rec<DevQuad>(S.quads_lds + (i << 7)), oo, dd, tmin, tmax, t);
+        } else {
+            const double a = __shfl(R.a, src), iao = __shfl(ia, src);
+            h = hit_sphere<false>(sphere_at<LS>(S, i), oo, dd, a, iao, tmin, tmax, 0.0, 0.0, t);
+        }
+        if (live && h) {
+            key[it] = static_cast<unsigned long long>(__double_as_longlong(t));  // t > t_min > 0
+            __hip_atomic_fetch_min(tkey + own[it], key[it], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (uint32_t it = 0; it < kCmpCap / 64; ++it)
+        if (key[it] != ~0ull && key[it] == tkey[own[it]])
+            __hip_atomic_fetch_min(best + own[it], idx[it], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    if (defer) {
+        const unsigned long long k = tkey[lane];
+        if (k != ~0ull) {
+            const double t = __longlong_as_double(static_cast<long long>(k));
+            R.tmax = t;
+            R.tmax32 = tmax_f32(t);
+            R.ref = (QUAD ? kRefQuad : 0u) | (R.first + best[lane]);
+            R.found = true;
+        }
+        R.state = R.sp < 0 ? kDone : kWalk;
+    }
 }
 
 __device__ __forceinline__ uint32_t owned_row(const Work& w, uint32_t k) {
@@ -1511,6 +1636,11 @@ __device__ __forceinline__ void stage_lds(unsigned char* dst, const void* src, u
 #ifndef CRT_SHADE_BATCH
 #define CRT_SHADE_BATCH 48
 #endif
+// pass 2 of the two-pass leaves by the whole wave over a compacted candidate list
+// (compact_candidates); 0: each lane tests its own candidates
+#ifndef CRT_COMPACT_CAND
+#define CRT_COMPACT_CAND 0
+#endif
 constexpr int kShadeBatch = CRT_SHADE_BATCH;
 // ...or once at least kShadeMin are and no more than kPendingMax lanes still traverse (off by
 // default: 56/32/8, 64/40/8 and 56/24/4 all measured slower than 48 alone)
@@ -1584,6 +1714,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W5 ? CRT
     // sqrt / reciprocal expansions without range fix-ups (sqrt_exact, recip_exact): measured
     // faster only in the five-wave sphere-only instance
     constexpr bool kFast = kSphOnly && W5;
+    // candidate compaction: the sphere-only and flat-parallelogram instances (their two-pass
+    // leaves); flat boxes are LDS-scene only
+    constexpr bool kCompact = CRT_COMPACT_CAND != 0 && (kSphOnly || (kFlatOnly && LSCENE));
     SceneView S = Sg;
     if (LSCENE) {  // f32 nodes at LDS offset 0 (fetch_nodef: a node's LDS address is its ref)
         if (static_cast<uint32_t>(reinterpret_cast<uintptr_t>((LdsByte*)smem)) != 0) __builtin_trap();
@@ -1782,7 +1915,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W5 ? CRT
                 if (wave_leader()) atomicAdd(&counters->round_leaves, nl);
             }
             if (COUNT) cl -= static_cast<uint32_t>(wall_clock64());
-            if (R.state == kLeaf) leaf_step<SE, COUNT, kTopTreelet && !LSCENE, LSCENE, kFast>(S, st, P.o, P.d, C.t_min, tmin32, kSphOnly || (!kFlatOnly && W.sphere_only != 0), !kFlatOnly && W.spheres_f32 != 0, kFlatOnly || (!kSphOnly && W.quads_f32 != 0), kFlatOnly || (!kSphOnly && W.quads_flat != 0), R, ctr);
+            uint32_t defer = 0;
+            if (R.state == kLeaf) defer = leaf_step<SE, COUNT, kTopTreelet && !LSCENE, LSCENE, kFast, kCompact>(S, st, P.o, P.d, C.t_min, tmin32, kSphOnly || (!kFlatOnly && W.sphere_only != 0), !kFlatOnly && W.spheres_f32 != 0, kFlatOnly || (!kSphOnly && W.quads_f32 != 0), kFlatOnly || (!kSphOnly && W.quads_flat != 0), R, ctr);
+            if (kCompact && __ballot(defer != 0) != 0)
+                compact_candidates<LSCENE, kFlatOnly, COUNT, kFast>(S, W.lds_cmp, P.o, P.d, C.t_min, defer, R, ctr);
             if (COUNT) cl += static_cast<uint32_t>(wall_clock64());
             const uint64_t pending = __ballot(R.state == kWalk);
             const uint64_t finished = __ballot(R.state == kDone);
@@ -2223,6 +2359,7 @@ static uint32_t count_owned(uint32_t h, uint32_t rb, uint32_t tc, uint32_t ti) {
 static size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
 
 constexpr size_t kAccBytes = CRT_ACC_LDS ? 3 * dev::kBlock * sizeof(double) : 0;  // five-wave sphere-only pixel sums
+constexpr size_t kCmpBytes = CRT_COMPACT_CAND ? (dev::kBlock / 64) * dev::kCmpWaveBytes : 0;  // compaction lists
 #ifndef CRT_FIVE_WAVES
 #define CRT_FIVE_WAVES 1
 #endif
@@ -2259,6 +2396,10 @@ static int launch_render(const crt_scene* s, int device, const crt_camera* cam, 
     if (W5 && PM == 0 && CRT_ACC_LDS) {  // then the pixel sums (render_kernel: kAccLds)
         W.lds_acc = static_cast<uint32_t>(align16(lds));
         lds = W.lds_acc + kAccBytes;
+    }
+    if (CRT_COMPACT_CAND && (PM == 0 || (PM == 2 && LSCENE))) {  // then the compaction lists
+        W.lds_cmp = static_cast<uint32_t>(align16(lds));
+        lds = W.lds_cmp + kCmpBytes;
     }
     const uint64_t pixels = static_cast<uint64_t>(W.owned_rows) * cam->image_w;
     // Sample chunks: a function of spp ONLY, so every pixel's sum is grouped identically whatever
@@ -2466,10 +2607,10 @@ static int dispatch_render(const crt_scene* s, int device, const crt_camera* cam
         // 3 116.5 vs 100.6 ms).
         const size_t budget5 = 160 * 1024 / CRT_MANY_WAVES;  // blocks of four waves a CU
         const bool w5 = (W.sphere_only || W.quads_flat) && kFiveWaves && std::getenv("CRT_FOUR_WAVES") == nullptr &&
-                        stack_at(scene_bytes) + stack_bytes + cam_bytes + (W.sphere_only ? kAccBytes : 0) <= budget5;
+                        stack_at(scene_bytes) + stack_bytes + cam_bytes + (W.sphere_only ? kAccBytes : 0) + kCmpBytes <= budget5;
         const size_t budget = w5 ? budget5 : kLdsSceneBudget;
         const uint32_t sph64 = static_cast<uint32_t>(s->spheres.size() * sizeof(DevSphere));
-        if (W.spheres_f32 && kSph64Lds && stack_at(scene_bytes + sph64) + stack_bytes + cam_bytes + (w5 ? kAccBytes : 0) <= budget)
+        if (W.spheres_f32 && kSph64Lds && stack_at(scene_bytes + sph64) + stack_bytes + cam_bytes + (w5 ? kAccBytes : 0) + kCmpBytes <= budget)
             W.bytes_sph64 = sph64;
         W.lds_stack = stack_at(scene_bytes + W.bytes_sph64);
         const size_t lds = W.lds_stack + stack_bytes;
@@ -2491,7 +2632,8 @@ static int dispatch_render(const crt_scene* s, int device, const crt_camera* cam
         return no_top ? 0u : static_cast<uint32_t>(std::min(all_nodes, room / sizeof(DevNodeF) * sizeof(DevNodeF)));
     };
     if (stack_bytes <= kLdsStackBudget && std::getenv("CRT_FORCE_GSTACK") == nullptr) {
-        const size_t room = per_block > stack_bytes + 2 * level ? per_block - stack_bytes - 2 * level : 0;
+        const size_t taken = stack_bytes + 2 * level + (W.sphere_only ? kCmpBytes : 0);
+        const size_t room = per_block > taken ? per_block - taken : 0;
         W.ntop = top_bytes(room);
         W.lds_nodes = 0;
         W.lds_stack = stack_at(align16(W.ntop));
