@@ -52,6 +52,10 @@ constexpr uint32_t kTileW = CRT_TILE_W, kTileH = 64 / CRT_TILE_W;
 #ifndef CRT_SPEC_MASKED
 #define CRT_SPEC_MASKED 1
 #endif
+// HBM-scene walks load both possible next nodes during the node test (walk())
+#ifndef CRT_WALK_PREFETCH
+#define CRT_WALK_PREFETCH 0
+#endif
 // the five-wave sphere-only instance keeps the lanes' pixel sums in LDS (render_kernel: kAccLds)
 #ifndef CRT_ACC_LDS
 #define CRT_ACC_LDS 1
@@ -86,6 +90,7 @@ struct SceneView {
     // through typed LDS pointers (ds_read, not flat); spheres_lds = ~0u when the spheres stay in HBM
     uint32_t refs_lds, spheres_lds, quads_lds;
     unsigned long long* guard;   // parity guard words (DeviceCopy::guard)
+    uint32_t sentinel;           // the sentinel's f32 ref, the largest valid one (render_kernel)
 };
 
 struct CamView {
@@ -409,6 +414,16 @@ __device__ __forceinline__ float vmax3(float a, float b, float c) {
     asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
     return r;
 }
+
+// the kernel's min / max for crt_quad_filter.h flat_box_candidate
+struct DevMinMax {
+    static __device__ __forceinline__ float min(float a, float b) { return vmin(a, b); }
+    static __device__ __forceinline__ float max(float a, float b) { return vmax(a, b); }
+    static __device__ __forceinline__ float min3(float a, float b, float c) { return vmin3(a, b, c); }
+    static __device__ __forceinline__ float max3(float a, float b, float c) { return vmax3(a, b, c); }
+    static __device__ __forceinline__ float max_s(float a, float b) { return vmax_s(a, b); }
+    static __device__ __forceinline__ float max_abs(float a, float b) { return vmax_abs(a, b); }
+};
 
 // The candidate filter of two-pass sphere leaves, two spheres per step in packed f32
 // (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32: one instruction for both spheres). It returns two
@@ -991,13 +1006,32 @@ __device__ __forceinline__ void walk(const SceneView& S, Stack<SE>& st, const do
         // one compare.
         bool run = true, nopend = true;
         uint32_t pref = ~0u, pcur = 0;
+        // HBM scenes (CRT_WALK_PREFETCH): the node the step moves to next is either the near child
+        // (entered interior node) or the stack top (anything else), and both references are known
+        // before the node test: both are loaded while the test runs, so the next step starts with
+        // its node in registers instead of waiting a memory latency after the test. A stack top
+        // below the guard level (garbage, never used) is clamped to a valid reference.
+        constexpr bool kPre = CRT_WALK_PREFETCH && TOP && !LS;
+        Uvec4 p0, p1;
+        if (kPre) fetch_nodef<TOP, LS>(S, cur, p0, p1);
         do {
             if (run) {
                 Uvec4 q0, q1;
-                fetch_nodef<TOP, LS>(S, cur, q0, q1);
+                if (kPre) {
+                    q0 = p0;
+                    q1 = p1;
+                } else {
+                    fetch_nodef<TOP, LS>(S, cur, q0, q1);
+                }
                 w0 = q1.z;
                 w1 = q1.w;
                 const uint32_t top = *tp;  // speculative pop
+                Uvec4 a0, a1, b0, b1;
+                if (kPre) {
+                    const uint32_t nr = w1 | (__builtin_amdgcn_ubfe(R.neg, w0, 1) << kNodeFShift);
+                    fetch_nodef<TOP, LS>(S, w1 < kLeafFlagF ? nr : cur, a0, a1);
+                    fetch_nodef<TOP, LS>(S, min(top, S.sentinel) & ~((1u << kNodeFShift) - 1), b0, b1);
+                }
                 if (COUNT) {
                     if (w1 != kSentinelW1) ctr.nodes++;
                     if (wave_leader()) ctr.it_walk++;
@@ -1031,6 +1065,10 @@ __device__ __forceinline__ void walk(const SceneView& S, Stack<SE>& st, const do
                 run = !park;
                 cur = inner ? near : top;
                 tp += inner ? stride : -stride;
+                if (kPre) {
+                    p0 = inner ? a0 : b0;
+                    p1 = inner ? a1 : b1;
+                }
             }
             nopend = pref == ~0u;
         } while (__ballot(nopend) != 0);
@@ -1229,16 +1267,9 @@ __device__ __forceinline__ uint32_t leaf_step(const SceneView& S, Stack<SE>& st,
             }
             LdsNodeF* p = (LdsNodeF*)static_cast<uintptr_t>(S.quadf_lds + ((range.x + i) << 5));
             const Uvec4 q0 = p->q0, q1 = p->q1;
-            const float x0 = __builtin_fmaf(__uint_as_float(q0.x), R.inv32[0], -R.oinv32[0]);
-            const float x1 = __builtin_fmaf(__uint_as_float(q0.y), R.inv32[0], -R.oinv32[0]);
-            const float y0 = __builtin_fmaf(__uint_as_float(q0.z), R.inv32[1], -R.oinv32[1]);
-            const float y1 = __builtin_fmaf(__uint_as_float(q0.w), R.inv32[1], -R.oinv32[1]);
-            const float z0 = __builtin_fmaf(__uint_as_float(q1.x), R.inv32[2], -R.oinv32[2]);
-            const float z1 = __builtin_fmaf(__uint_as_float(q1.y), R.inv32[2], -R.oinv32[2]);
-            const float lo = vmax3(vmin(x0, x1), vmin(y0, y1), vmax_s(vmin(z0, z1), tmin32));
-            const float hi = vmin3(vmax(x0, x1), vmax(y0, y1), vmin(vmax(z0, z1), R.tmax32));
-            const float th = __builtin_fmaf(vmax_abs(lo, hi), 0x1p-19f, R.marg);
-            cand |= static_cast<uint32_t>(!(hi - lo < -th)) << i;
+            const float b[6] = {__uint_as_float(q0.x), __uint_as_float(q0.y), __uint_as_float(q0.z),
+                                __uint_as_float(q0.w), __uint_as_float(q1.x), __uint_as_float(q1.y)};
+            cand |= static_cast<uint32_t>(flat_box_candidate<DevMinMax>(b, R.inv32, R.oinv32, tmin32, R.tmax32, R.marg)) << i;
         }
         if (CMP && cand) return cand;
         while (cand) {
@@ -1718,6 +1749,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W5 ? CRT
     // leaves); flat boxes are LDS-scene only
     constexpr bool kCompact = CRT_COMPACT_CAND != 0 && (kSphOnly || (kFlatOnly && LSCENE));
     SceneView S = Sg;
+    S.sentinel = W.sentinel;
     if (LSCENE) {  // f32 nodes at LDS offset 0 (fetch_nodef: a node's LDS address is its ref)
         if (static_cast<uint32_t>(reinterpret_cast<uintptr_t>((LdsByte*)smem)) != 0) __builtin_trap();
         stage_lds(smem, Sg.fnodes, W.bytes_nodes);

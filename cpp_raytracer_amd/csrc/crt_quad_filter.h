@@ -174,7 +174,8 @@ CRT_HD bool quad_candidate(const DevQuadF& q, const QuadRay32& L, Rcp rcp) {
 // the bounding slab values and |v_i / d_i| <= |slab value| + A are all <= M + A where they
 // decide), so the reference misses it too, for this t_max and any smaller one. Rays outside the
 // walk's range carry marg = inf (every quad a candidate), and NaN never rejects.
-// tools/fuzz_quad_filter.cpp runs this sequence against the exact test.
+// flat_box_candidate below is that sequence; the kernel (leaf_step) and tools/fuzz_quad_filter.cpp
+// (against the exact test) both call it.
 struct alignas(16) DevQuadBox {
     float b[6];      // x.min x.max y.min y.max z.min z.max (RN32 of the f64 bounds)
     uint32_t pad[2];
@@ -208,5 +209,35 @@ inline bool quad_flat_box(const double v[3], const double s1[3], const double s2
     f.pad[0] = f.pad[1] = 0;
     return true;
 }
+
+// The flat-box filter: false only where the exact test provably misses (see above). b = the box
+// (DevQuadBox::b), inv32 / oinv32 / marg = the ray's f32 walk constants (crt_device.hip
+// trav_init), tmin32 = RN32(t_min), tmax32 = RN32(min(t_max, 2^100)). MM supplies min / max /
+// min3 / max3 / max_s (second operand wave-uniform) / max_abs of non-NaN floats: the kernel's
+// v_min_f32 family, or std::fmin / std::fmax on the host (the same values for non-NaN operands).
+template <typename MM>
+CRT_HD bool flat_box_candidate(const float b[6], const float inv32[3], const float oinv32[3], float tmin32,
+                               float tmax32, float marg) {
+    const float x0 = std::fma(b[0], inv32[0], -oinv32[0]);
+    const float x1 = std::fma(b[1], inv32[0], -oinv32[0]);
+    const float y0 = std::fma(b[2], inv32[1], -oinv32[1]);
+    const float y1 = std::fma(b[3], inv32[1], -oinv32[1]);
+    const float z0 = std::fma(b[4], inv32[2], -oinv32[2]);
+    const float z1 = std::fma(b[5], inv32[2], -oinv32[2]);
+    const float lo = MM::max3(MM::min(x0, x1), MM::min(y0, y1), MM::max_s(MM::min(z0, z1), tmin32));
+    const float hi = MM::min3(MM::max(x0, x1), MM::max(y0, y1), MM::min(MM::max(z0, z1), tmax32));
+    const float th = std::fma(MM::max_abs(lo, hi), 0x1p-19f, marg);
+    return !(hi - lo < -th);
+}
+
+// host min / max for flat_box_candidate
+struct HostMinMax {
+    static float min(float a, float b) { return std::fmin(a, b); }
+    static float max(float a, float b) { return std::fmax(a, b); }
+    static float min3(float a, float b, float c) { return std::fmin(std::fmin(a, b), c); }
+    static float max3(float a, float b, float c) { return std::fmax(std::fmax(a, b), c); }
+    static float max_s(float a, float b) { return std::fmax(a, b); }
+    static float max_abs(float a, float b) { return std::fmax(std::fabs(a), std::fabs(b)); }
+};
 
 }  // namespace crt

@@ -93,9 +93,11 @@ static void rand_dir(double s, double d[3]) {
 static long viol = 0, miss_total = 0, miss_rejected = 0, hits = 0, skipped = 0;
 static long fviol = 0, fmiss_total = 0, fmiss_rejected = 0, fhits = 0;
 
-// the render kernel's flat-box filter for axis-aligned parallelograms (crt_device.hip leaf_step):
-// the walk's f32 node test, with the ray constants of trav_init (inv32 = v_rcp_f32(RN32(d)),
-// oinv32 = RN32(RN32(o) inv32), marg) and tmin' = RN32(t_min), tmax' = RN32(min(t_max, 2^100))
+// the render kernel's flat-box filter for axis-aligned parallelograms (crt_device.hip leaf_step
+// calls the same crt::flat_box_candidate), with the ray constants of trav_init (inv32 =
+// v_rcp_f32(RN32(d)), oinv32 = RN32(RN32(o) inv32), marg) and tmin' = RN32(t_min),
+// tmax' = RN32(min(t_max, 2^100)). The walk's range (|d'_k| in [2^-39, 2^39], |o'_k| <= 2^40) is
+// the filter's own; outside it marg = inf keeps every parallelogram.
 static bool flat_candidate(const crt::DevQuadBox& b, const double o[3], const double d[3], double tmin,
                            double tmax) {
     float inv[3], oinv[3], A = 0;
@@ -109,21 +111,14 @@ static bool flat_candidate(const crt::DevQuadBox& b, const double o[3], const do
     }
     const float marg = f32 ? std::fmax(A * 0x1p-19f, 0x1p-60f) : INFINITY;
     const float tmin32 = static_cast<float>(tmin), tmax32 = static_cast<float>(std::fmin(tmax, 0x1p100));
-    float t[6];
-    for (int j = 0; j < 6; ++j) t[j] = std::fma(b.b[j], inv[j / 2], -oinv[j / 2]);
-    const float lo = std::fmax(std::fmax(std::fmin(t[0], t[1]), std::fmin(t[2], t[3])), std::fmax(std::fmin(t[4], t[5]), tmin32));
-    const float hi = std::fmin(std::fmin(std::fmax(t[0], t[1]), std::fmax(t[2], t[3])), std::fmin(std::fmax(t[4], t[5]), tmax32));
-    const float th = std::fma(std::fmax(std::fabs(lo), std::fabs(hi)), 0x1p-19f, marg);
-    return !(hi - lo < -th);
+    return crt::flat_box_candidate<crt::HostMinMax>(b.b, inv, oinv, tmin32, tmax32, marg);
 }
 
+static long fwide = 0;  // flat cases outside the generic filter's range (quad_ray32_ok false)
+
 static void check(const Quad& q, const double o[3], const double d[3], double tmin, double tmax) {
-    DevQuadF f;
-    if (!record(q, f) || !crt::quad_ray32_ok(o, d)) { ++skipped; return; }
-    QuadRay32 L;
-    crt::quad_ray32(o, d, tmin, tmax, L);
-    const bool cand = crt::quad_candidate(f, L, rcp_adversarial);
     const bool hit = exact(q, o, d, tmin, tmax, nullptr);
+    // the flat-box filter first: its range is the walk's, not the generic filter's
     crt::DevQuadBox box;
     if (crt::quad_flat_box(q.v, q.s1, q.s2, box)) {
         const bool fc = flat_candidate(box, o, d, tmin, tmax);
@@ -137,7 +132,13 @@ static void check(const Quad& q, const double o[3], const double d[3], double tm
             ++fmiss_total;
             fmiss_rejected += !fc;
         }
+        if (!crt::quad_ray32_ok(o, d)) ++fwide;
     }
+    DevQuadF f;
+    if (!record(q, f) || !crt::quad_ray32_ok(o, d)) { ++skipped; return; }
+    QuadRay32 L;
+    crt::quad_ray32(o, d, tmin, tmax, L);
+    const bool cand = crt::quad_candidate(f, L, rcp_adversarial);
     if (hit) {
         ++hits;
         if (!cand) {
@@ -230,11 +231,26 @@ int main(int argc, char** argv) {
         rand_dir(urange(0.2, 2), d);
         check(q, o, d, tmin, u01() < 0.5 ? INFINITY : urange(1, 2000));
     }
+    for (long i = 0; i < M; ++i) {  // the walk's range edges: |o| up to 2^40, |d_k| from 2^-39 to 2^39
+        const double S = std::exp2(urange(20, 38));
+        Quad q = rand_quad(S);
+        double o[3], d[3];
+        for (int k = 0; k < 3; ++k) o[k] = urange(-1, 1) * std::exp2(urange(30, 40));
+        for (int k = 0; k < 3; ++k) d[k] = (u01() < 0.5 ? -1 : 1) * std::exp2(urange(-39, 39));
+        if (u01() < 0.5) {  // aimed at the rectangle (or just past an edge)
+            double p[3];
+            point_on(q, urange(-0.01, 1.01), urange(-0.01, 1.01), p);
+            const double t0 = std::exp2(urange(-20, 20));
+            for (int k = 0; k < 3; ++k) o[k] = std::fmax(-0x1p40, std::fmin(0x1p40, p[k] - d[k] * t0));
+        }
+        const double tmax = u01() < 0.5 ? INFINITY : std::exp2(urange(-30, 60));
+        check(q, o, d, tmin, tmax);
+    }
     std::printf("cases %ld (skipped %ld): exact hits %ld, violations %ld; exact misses %ld, rejected by the "
-                "filter %.4f\n", 5 * M, skipped, hits, viol, miss_total,
+                "filter %.4f\n", 6 * M, skipped, hits, viol, miss_total,
                 miss_total ? static_cast<double>(miss_rejected) / miss_total : 0.0);
     std::printf("flat-box filter (axis-aligned parallelograms): exact hits %ld, violations %ld; exact misses %ld, "
-                "rejected %.4f\n", fhits, fviol, fmiss_total,
-                fmiss_total ? static_cast<double>(fmiss_rejected) / fmiss_total : 0.0);
+                "rejected %.4f; %ld of them outside the generic filter's range\n", fhits, fviol, fmiss_total,
+                fmiss_total ? static_cast<double>(fmiss_rejected) / fmiss_total : 0.0, fwide);
     return viol != 0 || fviol != 0;
 }
