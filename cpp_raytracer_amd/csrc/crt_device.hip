@@ -52,10 +52,6 @@ constexpr uint32_t kTileW = CRT_TILE_W, kTileH = 64 / CRT_TILE_W;
 #ifndef CRT_SPEC_MASKED
 #define CRT_SPEC_MASKED 1
 #endif
-// HBM-scene walks load both possible next nodes during the node test (walk())
-#ifndef CRT_WALK_PREFETCH
-#define CRT_WALK_PREFETCH 0
-#endif
 // the five-wave sphere-only instance keeps the lanes' pixel sums in LDS (render_kernel: kAccLds)
 #ifndef CRT_ACC_LDS
 #define CRT_ACC_LDS 1
@@ -90,7 +86,6 @@ struct SceneView {
     // through typed LDS pointers (ds_read, not flat); spheres_lds = ~0u when the spheres stay in HBM
     uint32_t refs_lds, spheres_lds, quads_lds;
     unsigned long long* guard;   // parity guard words (DeviceCopy::guard)
-    uint32_t sentinel;           // the sentinel's f32 ref, the largest valid one (render_kernel)
 };
 
 struct CamView {
@@ -1006,32 +1001,13 @@ __device__ __forceinline__ void walk(const SceneView& S, Stack<SE>& st, const do
         // one compare.
         bool run = true, nopend = true;
         uint32_t pref = ~0u, pcur = 0;
-        // HBM scenes (CRT_WALK_PREFETCH): the node the step moves to next is either the near child
-        // (entered interior node) or the stack top (anything else), and both references are known
-        // before the node test: both are loaded while the test runs, so the next step starts with
-        // its node in registers instead of waiting a memory latency after the test. A stack top
-        // below the guard level (garbage, never used) is clamped to a valid reference.
-        constexpr bool kPre = CRT_WALK_PREFETCH && TOP && !LS;
-        Uvec4 p0, p1;
-        if (kPre) fetch_nodef<TOP, LS>(S, cur, p0, p1);
         do {
             if (run) {
                 Uvec4 q0, q1;
-                if (kPre) {
-                    q0 = p0;
-                    q1 = p1;
-                } else {
-                    fetch_nodef<TOP, LS>(S, cur, q0, q1);
-                }
+                fetch_nodef<TOP, LS>(S, cur, q0, q1);
                 w0 = q1.z;
                 w1 = q1.w;
                 const uint32_t top = *tp;  // speculative pop
-                Uvec4 a0, a1, b0, b1;
-                if (kPre) {
-                    const uint32_t nr = w1 | (__builtin_amdgcn_ubfe(R.neg, w0, 1) << kNodeFShift);
-                    fetch_nodef<TOP, LS>(S, w1 < kLeafFlagF ? nr : cur, a0, a1);
-                    fetch_nodef<TOP, LS>(S, min(top, S.sentinel) & ~((1u << kNodeFShift) - 1), b0, b1);
-                }
                 if (COUNT) {
                     if (w1 != kSentinelW1) ctr.nodes++;
                     if (wave_leader()) ctr.it_walk++;
@@ -1065,10 +1041,6 @@ __device__ __forceinline__ void walk(const SceneView& S, Stack<SE>& st, const do
                 run = !park;
                 cur = inner ? near : top;
                 tp += inner ? stride : -stride;
-                if (kPre) {
-                    p0 = inner ? a0 : b0;
-                    p1 = inner ? a1 : b1;
-                }
             }
             nopend = pref == ~0u;
         } while (__ballot(nopend) != 0);
@@ -1749,7 +1721,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W5 ? CRT
     // leaves); flat boxes are LDS-scene only
     constexpr bool kCompact = CRT_COMPACT_CAND != 0 && (kSphOnly || (kFlatOnly && LSCENE));
     SceneView S = Sg;
-    S.sentinel = W.sentinel;
     if (LSCENE) {  // f32 nodes at LDS offset 0 (fetch_nodef: a node's LDS address is its ref)
         if (static_cast<uint32_t>(reinterpret_cast<uintptr_t>((LdsByte*)smem)) != 0) __builtin_trap();
         stage_lds(smem, Sg.fnodes, W.bytes_nodes);
