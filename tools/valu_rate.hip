@@ -8,6 +8,7 @@
 //   tools/build/valu_rate  -> one JSON line
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <vector>
 
@@ -31,7 +32,7 @@ constexpr int kUnroll = 16;
                  : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7))
 
 template <int KIND, typename T>
-__global__ void rate_kernel(unsigned long long* cycles, T* sink, T seed) {
+__global__ __launch_bounds__(1024) void rate_kernel(unsigned long long* cycles, T* sink, T seed) {
     T a0 = seed, a1 = seed + 1, a2 = seed + 2, a3 = seed + 3, a4 = seed + 4, a5 = seed + 5, a6 = seed + 6,
       a7 = seed + 7, b = seed * T(0.5);
     __syncthreads();
@@ -53,25 +54,39 @@ __global__ void rate_kernel(unsigned long long* cycles, T* sink, T seed) {
     if ((threadIdx.x & 63) == 0) cycles[(blockIdx.x * blockDim.x + threadIdx.x) >> 6] = t1 - t0;
 }
 
+// waves per SIMD: `blocks_per_cu` blocks of `threads` on every CU, their waves dealt over the 4
+// SIMDs. Returns memtime ticks per instruction per SIMD, and (via ghz) the memtime tick rate
+// against the launch's wall time.
 template <int KIND, typename T>
-static double measure(int blocks, int threads) {
+static double measure(int cus, int threads, int blocks_per_cu, double* ghz) {
+    const int blocks = cus * blocks_per_cu;
     const int waves = blocks * threads / 64;
     unsigned long long* d_cyc = nullptr;
     T* d_sink = nullptr;
     if (hipMalloc(&d_cyc, waves * sizeof(unsigned long long)) != hipSuccess) return -1;
     if (hipMalloc(&d_sink, static_cast<size_t>(blocks) * threads * sizeof(T)) != hipSuccess) return -1;
-    for (int rep = 0; rep < 2; ++rep)  // the first launch warms up clocks and code
-        hipLaunchKernelGGL((rate_kernel<KIND, T>), dim3(blocks), dim3(threads), 0, 0, d_cyc, d_sink, T(1.0001));
+    hipEvent_t e0, e1;
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    hipLaunchKernelGGL((rate_kernel<KIND, T>), dim3(blocks), dim3(threads), 0, 0, d_cyc, d_sink, T(1.0001));  // warm-up
+    (void)hipEventRecord(e0, 0);
+    hipLaunchKernelGGL((rate_kernel<KIND, T>), dim3(blocks), dim3(threads), 0, 0, d_cyc, d_sink, T(1.0001));
+    (void)hipEventRecord(e1, 0);
     if (hipDeviceSynchronize() != hipSuccess) return -1;
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, e0, e1);
     std::vector<unsigned long long> cyc(waves);
     if (hipMemcpy(cyc.data(), d_cyc, waves * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess) return -1;
     (void)hipFree(d_cyc);
     (void)hipFree(d_sink);
-    double mean = 0;
-    for (auto c : cyc) mean += static_cast<double>(c);
+    double mean = 0, mx = 0;
+    for (auto c : cyc) {
+        mean += static_cast<double>(c);
+        mx = std::max(mx, static_cast<double>(c));
+    }
     mean /= waves;
-    // waves per SIMD: a block of `threads` lands on one CU, its waves dealt over the 4 SIMDs
-    const double per_simd = (threads / 64) / 4.0;
+    if (ghz) *ghz = mx / (ms * 1e6);
+    const double per_simd = (threads / 64) * blocks_per_cu / 4.0;
     return mean / (per_simd * kIters * kUnroll);
 }
 
@@ -79,19 +94,26 @@ int main() {
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0) != hipSuccess) return 1;
     const char* names[] = {"v_fma_f32", "v_add_f64", "v_mul_f64", "v_fma_f64", "v_rcp_f64", "v_add_f32"};
-    std::printf("{\"cus\": %d, \"cycles_per_wave64_instruction\": {", cus);
+    const int cfg[4][2] = {{256, 1}, {512, 1}, {1024, 1}, {1024, 2}};  // 1, 2, 4, 8 waves per SIMD
+    double ghz = 0;
+    std::printf("{\"cus\": %d, \"memtime_ticks_per_wave64_instruction_per_simd\": {", cus);
     for (int k = 0; k < 6; ++k) {
-        double c1 = 0, c2 = 0;
-        switch (k) {
-            case 0: c1 = measure<0, float>(cus, 256); c2 = measure<0, float>(cus, 512); break;
-            case 1: c1 = measure<1, double>(cus, 256); c2 = measure<1, double>(cus, 512); break;
-            case 2: c1 = measure<2, double>(cus, 256); c2 = measure<2, double>(cus, 512); break;
-            case 3: c1 = measure<3, double>(cus, 256); c2 = measure<3, double>(cus, 512); break;
-            case 4: c1 = measure<4, double>(cus, 256); c2 = measure<4, double>(cus, 512); break;
-            case 5: c1 = measure<5, float>(cus, 256); c2 = measure<5, float>(cus, 512); break;
+        std::printf("%s\"%s\": {", k ? ", " : "", names[k]);
+        for (int c = 0; c < 4; ++c) {
+            double r = 0;
+            const int th = cfg[c][0], bp = cfg[c][1];
+            switch (k) {
+                case 0: r = measure<0, float>(cus, th, bp, &ghz); break;
+                case 1: r = measure<1, double>(cus, th, bp, &ghz); break;
+                case 2: r = measure<2, double>(cus, th, bp, &ghz); break;
+                case 3: r = measure<3, double>(cus, th, bp, &ghz); break;
+                case 4: r = measure<4, double>(cus, th, bp, &ghz); break;
+                case 5: r = measure<5, float>(cus, th, bp, &ghz); break;
+            }
+            std::printf("%s\"%d_waves\": %.3f", c ? ", " : "", th / 64 * bp / 4, r);
         }
-        std::printf("%s\"%s\": {\"1_wave_per_simd\": %.3f, \"2_waves_per_simd\": %.3f}", k ? ", " : "", names[k], c1, c2);
+        std::printf("}");
     }
-    std::printf("}}\n");
+    std::printf("}, \"memtime_ghz_vs_wall\": %.3f}\n", ghz);
     return 0;
 }
