@@ -32,10 +32,11 @@ constexpr int kUnroll = 16;
                  : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7))
 
 template <int KIND, typename T>
-__global__ __launch_bounds__(1024) void rate_kernel(unsigned long long* cycles, T* sink, T seed) {
+__global__ __launch_bounds__(1024) void rate_kernel(unsigned long long* cycles, unsigned long long* real, T* sink, T seed) {
     T a0 = seed, a1 = seed + 1, a2 = seed + 2, a3 = seed + 3, a4 = seed + 4, a5 = seed + 5, a6 = seed + 6,
       a7 = seed + 7, b = seed * T(0.5);
     __syncthreads();
+    const unsigned long long r0 = __builtin_amdgcn_s_memrealtime();
     const unsigned long long t0 = __builtin_amdgcn_s_memtime();
     for (int i = 0; i < kIters; ++i) {
 #pragma unroll
@@ -49,43 +50,52 @@ __global__ __launch_bounds__(1024) void rate_kernel(unsigned long long* cycles, 
         }
     }
     const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    const unsigned long long r1 = __builtin_amdgcn_s_memrealtime();
     // every lane writes (vector stores): the chains stay live
     sink[blockIdx.x * blockDim.x + threadIdx.x] = a0 + a1 + a2 + a3 + a4 + a5 + a6 + a7;
-    if ((threadIdx.x & 63) == 0) cycles[(blockIdx.x * blockDim.x + threadIdx.x) >> 6] = t1 - t0;
+    if ((threadIdx.x & 63) == 0) {
+        cycles[(blockIdx.x * blockDim.x + threadIdx.x) >> 6] = t1 - t0;
+        real[(blockIdx.x * blockDim.x + threadIdx.x) >> 6] = r1 - r0;  // 100 MHz
+    }
 }
 
 // waves per SIMD: `blocks_per_cu` blocks of `threads` on every CU, their waves dealt over the 4
 // SIMDs. Returns memtime ticks per instruction per SIMD, and (via ghz) the memtime tick rate
-// against the launch's wall time.
+// against s_memrealtime (a constant 100 MHz) over the waves' own spans: the shader clock the
+// ticks run at.
 template <int KIND, typename T>
 static double measure(int cus, int threads, int blocks_per_cu, double* ghz) {
     const int blocks = cus * blocks_per_cu;
     const int waves = blocks * threads / 64;
-    unsigned long long* d_cyc = nullptr;
+    unsigned long long *d_cyc = nullptr, *d_real = nullptr;
     T* d_sink = nullptr;
     if (hipMalloc(&d_cyc, waves * sizeof(unsigned long long)) != hipSuccess) return -1;
+    if (hipMalloc(&d_real, waves * sizeof(unsigned long long)) != hipSuccess) return -1;
     if (hipMalloc(&d_sink, static_cast<size_t>(blocks) * threads * sizeof(T)) != hipSuccess) return -1;
     hipEvent_t e0, e1;
     (void)hipEventCreate(&e0);
     (void)hipEventCreate(&e1);
-    hipLaunchKernelGGL((rate_kernel<KIND, T>), dim3(blocks), dim3(threads), 0, 0, d_cyc, d_sink, T(1.0001));  // warm-up
+    hipLaunchKernelGGL((rate_kernel<KIND, T>), dim3(blocks), dim3(threads), 0, 0, d_cyc, d_real, d_sink, T(1.0001));  // warm-up
     (void)hipEventRecord(e0, 0);
-    hipLaunchKernelGGL((rate_kernel<KIND, T>), dim3(blocks), dim3(threads), 0, 0, d_cyc, d_sink, T(1.0001));
+    hipLaunchKernelGGL((rate_kernel<KIND, T>), dim3(blocks), dim3(threads), 0, 0, d_cyc, d_real, d_sink, T(1.0001));
     (void)hipEventRecord(e1, 0);
     if (hipDeviceSynchronize() != hipSuccess) return -1;
     float ms = 0;
     (void)hipEventElapsedTime(&ms, e0, e1);
-    std::vector<unsigned long long> cyc(waves);
+    std::vector<unsigned long long> cyc(waves), rt(waves);
     if (hipMemcpy(cyc.data(), d_cyc, waves * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    if (hipMemcpy(rt.data(), d_real, waves * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess) return -1;
     (void)hipFree(d_cyc);
+    (void)hipFree(d_real);
     (void)hipFree(d_sink);
-    double mean = 0, mx = 0;
-    for (auto c : cyc) {
-        mean += static_cast<double>(c);
-        mx = std::max(mx, static_cast<double>(c));
+    double mean = 0, sum_rt = 0;
+    for (int i = 0; i < waves; ++i) {
+        mean += static_cast<double>(cyc[i]);
+        sum_rt += static_cast<double>(rt[i]);
     }
+    // memtime ticks per ns of the constant 100 MHz clock, over the waves' own spans
+    if (ghz) *ghz = mean / (sum_rt * 10.0);
     mean /= waves;
-    if (ghz) *ghz = mx / (ms * 1e6);
     const double per_simd = (threads / 64) * blocks_per_cu / 4.0;
     return mean / (per_simd * kIters * kUnroll);
 }
@@ -114,6 +124,6 @@ int main() {
         }
         std::printf("}");
     }
-    std::printf("}, \"memtime_ghz_vs_wall\": %.3f}\n", ghz);
+    std::printf("}, \"memtime_ghz_vs_memrealtime\": %.3f}\n", ghz);
     return 0;
 }
