@@ -19,8 +19,9 @@ P1=$(pick FETCH_SIZE GRBM_GUI_ACTIVE)
 P2=$(pick WRITE_SIZE TCC_HIT_sum TCC_MISS_sum)
 P3=$(pick SQ_INSTS_VALU SQ_BUSY_CYCLES SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU)
 P4=$(pick SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVES SQ_LDS_BANK_CONFLICT)
+P5=$(pick SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_CVT SQ_INSTS_VALU)
 i=0
-for grp in "$P1" "$P2" "$P3" "$P4"; do
+for grp in "$P1" "$P2" "$P3" "$P4" "$P5"; do
   i=$((i+1))
   [ -n "$grp" ] || continue
   timeout -s KILL 240 rocprofv3 --pmc $grp --kernel-trace --output-format csv -d "$OUT/p$i" -o run -- python3 "$R/bench.py" $ARGS > "$OUT/bench_p$i.json" 2> "$OUT/bench_p$i.err" || { echo "pmc pass $i ($grp) failed"; tail -5 "$OUT/bench_p$i.err"; exit 1; }

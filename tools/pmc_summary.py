@@ -6,11 +6,21 @@ gfx950 by 2x, so HBM read bytes = 2 * FETCH_SIZE * 1024; WRITE_SIZE (KB) is take
 counter group ran in its own rocprofv3 --pmc pass. Values are averaged over the launches of the
 timed render kernel (template COUNT = false; the instrumented pass is excluded).
 
-VALU issue (a MODEL ESTIMATE, pinned by tools/valu_rate.hip): a wave64 VALU instruction occupies
-its SIMD for 2 cycles, an f64 one for 4; SQ_BUSY_CYCLES sums busy cycles over the 32 SQs (8 XCDs x
-4 shader engines), so the chip's SIMD-cycles are 32 x SQ_BUSY_CYCLES (1024 SIMDs). Model-free
-cross-checks from the same passes: the SIMD-cycles from GRBM_GUI_ACTIVE (summed over 8 XCDs:
-1024 x GRBM_GUI_ACTIVE / 8) and the effective clock GRBM_GUI_ACTIVE / 8 / kernel time.
+VALU issue. SQ_BUSY_CYCLES sums busy cycles over the 32 SQs (8 XCDs x 4 shader engines), so the
+chip's SIMD-cycles are 32 x SQ_BUSY_CYCLES (1024 SIMDs); the model-free cross-check is the
+SIMD-cycles from GRBM_GUI_ACTIVE (summed over 8 XCDs: 1024 x GRBM_GUI_ACTIVE / 8), which also gives
+the effective clock GRBM_GUI_ACTIVE / 8 / kernel time. Issue cycles two ways:
+  valu_issue_frac_model     2 cycles per wave64 VALU instruction, 4 per f64 one (the textbook
+                            SIMD-32 model; the round-2 figure)
+  valu_issue_frac_measured  each instruction class (SQ_INSTS_VALU_* counters, pass 5) at the
+                            SIMD cycles per wave64 instruction tools/valu_rate.hip measured on the
+                            MI355X (profiles/r03_v3/valu_rate.json: wall time x shader clock over
+                            each SIMD's instructions, 8 waves per SIMD, loop overhead included):
+                            f32 add / mul / fma and int32 2.30-2.41 (nominal 2), f64 add / mul /
+                            fma 4.15-4.18 (nominal 4), f32 transcendental 8.16 (8), f64
+                            transcendental 16.16 (16). The summary uses the nominal values the
+                            measurement confirms; CVT and int64 count as f64-class (4), every
+                            other VALU instruction (moves, selects, compares, packed f32) as 2.
 
 usage: python tools/pmc_summary.py <pmc dir> <out.json> [workload]
 The workload key defaults to config.workload of <dir>/bench_p1.json (the bench line of pass 1);
@@ -70,11 +80,22 @@ def main():
     f64 = ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_TRANS_F64")
     if "SQ_INSTS_VALU" in avg and "SQ_BUSY_CYCLES" in avg and all(k in avg for k in f64):
         n64 = sum(avg[k] for k in f64)
-        res["valu_issue_cycles"] = 2 * avg["SQ_INSTS_VALU"] + 2 * n64
+        res["valu_issue_cycles_model"] = 2 * avg["SQ_INSTS_VALU"] + 2 * n64
         res["simd_cycles"] = 32 * avg["SQ_BUSY_CYCLES"]
-        res["valu_issue_frac"] = res["valu_issue_cycles"] / res["simd_cycles"]
-        res["valu_issue_model"] = "estimate: 2 cycles per wave64 VALU instruction, 4 per f64 (tools/valu_rate.hip)"
+        res["valu_issue_frac_model"] = res["valu_issue_cycles_model"] / res["simd_cycles"]
         res["valu_insts_per_simd_cycle"] = avg["SQ_INSTS_VALU"] / res["simd_cycles"]
+        cls = {"SQ_INSTS_VALU_ADD_F32": 2, "SQ_INSTS_VALU_MUL_F32": 2, "SQ_INSTS_VALU_INT32": 2,
+               "SQ_INSTS_VALU_FMA_F32": 2, "SQ_INSTS_VALU_CVT": 4, "SQ_INSTS_VALU_TRANS_F32": 8,
+               "SQ_INSTS_VALU_ADD_F64": 4, "SQ_INSTS_VALU_MUL_F64": 4, "SQ_INSTS_VALU_FMA_F64": 4,
+               "SQ_INSTS_VALU_INT64": 4, "SQ_INSTS_VALU_TRANS_F64": 16}
+        if all(k in avg for k in cls):
+            other = avg["SQ_INSTS_VALU"] - sum(avg[k] for k in cls)
+            res["valu_issue_cycles_measured"] = sum(avg[k] * c for k, c in cls.items()) + 2 * max(0.0, other)
+            res["valu_other_insts"] = other
+            res["valu_issue_frac_measured"] = res["valu_issue_cycles_measured"] / res["simd_cycles"]
+        res["valu_issue_frac"] = res.get("valu_issue_frac_measured", res["valu_issue_frac_model"])
+        res["valu_issue_basis"] = ("per-class costs measured by tools/valu_rate.hip" if "valu_issue_frac_measured" in res
+                                   else "model: 2 cycles per wave64 instruction, 4 per f64")
     if "GRBM_GUI_ACTIVE" in avg:
         res["simd_cycles_from_grbm"] = 1024 * avg["GRBM_GUI_ACTIVE"] / 8
         if durs:

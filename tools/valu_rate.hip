@@ -1,9 +1,8 @@
 // Microbenchmark pinning the VALU issue model of tools/pmc_summary.py on the MI355X: the SIMD
 // cycles one wave64 VALU instruction occupies, for the instruction kinds the render kernel issues
-// (f32 fma, f64 add / mul / fma, f64 reciprocal), measured with s_memtime (shader clock) inside
-// each wave. Every wave runs 8 independent accumulator chains (latency hidden by ILP) of
-// kIters x 16 instructions; with w waves on one SIMD the SIMD's issue cost per instruction is
-// elapsed_cycles / (w x instructions per wave).
+// (f32 add / mul / fma / rcp, int32, f64 add / mul / fma / rcp), from the wall time of grids with
+// 1, 2, 4 and 8 waves per SIMD at the shader clock (s_memtime against s_memrealtime). Every wave
+// runs 8 independent accumulator chains (latency hidden by ILP) of kIters x 16 instructions.
 //   hipcc --offload-arch=gfx950 -O3 tools/valu_rate.hip -o tools/build/valu_rate
 //   tools/build/valu_rate  -> one JSON line
 #include <hip/hip_runtime.h>
@@ -21,11 +20,11 @@ constexpr int kUnroll = 16;
                  : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7)  \
                  : "v"(b))
 #define CHAIN8_FMA(OP)                                                                                   \
-    asm volatile(OP " %0, %0, %8, %8\n\t" OP " %1, %1, %8, %8\n\t" OP " %2, %2, %8, %8\n\t"              \
-                 OP " %3, %3, %8, %8\n\t" OP " %4, %4, %8, %8\n\t" OP " %5, %5, %8, %8\n\t"              \
-                 OP " %6, %6, %8, %8\n\t" OP " %7, %7, %8, %8"                                           \
+    asm volatile(OP " %0, %0, %8, %9\n\t" OP " %1, %1, %8, %9\n\t" OP " %2, %2, %8, %9\n\t"              \
+                 OP " %3, %3, %8, %9\n\t" OP " %4, %4, %8, %9\n\t" OP " %5, %5, %8, %9\n\t"              \
+                 OP " %6, %6, %8, %9\n\t" OP " %7, %7, %8, %9"                                           \
                  : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7)      \
-                 : "v"(b))
+                 : "v"(b), "v"(c))
 #define CHAIN8_UN(OP)                                                                            \
     asm volatile(OP " %0, %0\n\t" OP " %1, %1\n\t" OP " %2, %2\n\t" OP " %3, %3\n\t"             \
                  OP " %4, %4\n\t" OP " %5, %5\n\t" OP " %6, %6\n\t" OP " %7, %7"                 \
@@ -34,7 +33,7 @@ constexpr int kUnroll = 16;
 template <int KIND, typename T>
 __global__ __launch_bounds__(1024) void rate_kernel(unsigned long long* cycles, unsigned long long* real, T* sink, T seed) {
     T a0 = seed, a1 = seed + 1, a2 = seed + 2, a3 = seed + 3, a4 = seed + 4, a5 = seed + 5, a6 = seed + 6,
-      a7 = seed + 7, b = seed * T(0.5);
+      a7 = seed + 7, b = seed * T(0.5), c = seed * T(0.25);
     __syncthreads();
     const unsigned long long r0 = __builtin_amdgcn_s_memrealtime();
     const unsigned long long t0 = __builtin_amdgcn_s_memtime();
@@ -47,6 +46,9 @@ __global__ __launch_bounds__(1024) void rate_kernel(unsigned long long* cycles, 
             if constexpr (KIND == 3) CHAIN8_FMA("v_fma_f64");
             if constexpr (KIND == 4) CHAIN8_UN("v_rcp_f64");
             if constexpr (KIND == 5) CHAIN8("v_add_f32");
+            if constexpr (KIND == 6) CHAIN8("v_mul_f32");
+            if constexpr (KIND == 7) CHAIN8("v_xor_b32");
+            if constexpr (KIND == 8) CHAIN8_UN("v_rcp_f32");
         }
     }
     const unsigned long long t1 = __builtin_amdgcn_s_memtime();
@@ -59,10 +61,11 @@ __global__ __launch_bounds__(1024) void rate_kernel(unsigned long long* cycles, 
     }
 }
 
-// waves per SIMD: `blocks_per_cu` blocks of `threads` on every CU, their waves dealt over the 4
-// SIMDs. Returns memtime ticks per instruction per SIMD, and (via ghz) the memtime tick rate
-// against s_memrealtime (a constant 100 MHz) over the waves' own spans: the shader clock the
-// ticks run at.
+// A grid of `blocks_per_cu` blocks of `threads` per CU. Returns the SIMD cycles per wave64
+// instruction: the launch's wall time (HIP events) x the shader clock over the instructions each
+// of the 1024 SIMDs executes; the clock is s_memtime against s_memrealtime (a constant 100 MHz)
+// over the waves' spans. Launch overhead is included (< 1% at these sizes).
+static double g_last_ms = 0;  // wall time of the last timed launch
 template <int KIND, typename T>
 static double measure(int cus, int threads, int blocks_per_cu, double* ghz) {
     const int blocks = cus * blocks_per_cu;
@@ -82,32 +85,36 @@ static double measure(int cus, int threads, int blocks_per_cu, double* ghz) {
     if (hipDeviceSynchronize() != hipSuccess) return -1;
     float ms = 0;
     (void)hipEventElapsedTime(&ms, e0, e1);
+    g_last_ms = ms;
     std::vector<unsigned long long> cyc(waves), rt(waves);
     if (hipMemcpy(cyc.data(), d_cyc, waves * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess) return -1;
     if (hipMemcpy(rt.data(), d_real, waves * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess) return -1;
     (void)hipFree(d_cyc);
     (void)hipFree(d_real);
     (void)hipFree(d_sink);
-    double mean = 0, sum_rt = 0;
+    double sum_t = 0, sum_rt = 0;
     for (int i = 0; i < waves; ++i) {
-        mean += static_cast<double>(cyc[i]);
+        sum_t += static_cast<double>(cyc[i]);
         sum_rt += static_cast<double>(rt[i]);
     }
-    // memtime ticks per ns of the constant 100 MHz clock, over the waves' own spans
-    if (ghz) *ghz = mean / (sum_rt * 10.0);
-    mean /= waves;
-    const double per_simd = (threads / 64) * blocks_per_cu / 4.0;
-    return mean / (per_simd * kIters * kUnroll);
+    // the shader clock: memtime ticks per ns of the constant 100 MHz clock, over the waves' spans
+    const double clk = sum_t / (sum_rt * 10.0);
+    if (ghz) *ghz = clk;
+    // cycles per wave64 instruction per SIMD from the launch's wall time (the waves' own spans
+    // would assume every wave of the grid resident at once, which the dispatch does not guarantee)
+    const double insts_per_simd = static_cast<double>(waves) * kIters * kUnroll / (cus * 4.0);
+    return ms * 1e-3 * clk * 1e9 / insts_per_simd;
 }
 
 int main() {
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0) != hipSuccess) return 1;
-    const char* names[] = {"v_fma_f32", "v_add_f64", "v_mul_f64", "v_fma_f64", "v_rcp_f64", "v_add_f32"};
+    const char* names[] = {"v_fma_f32", "v_add_f64", "v_mul_f64", "v_fma_f64", "v_rcp_f64", "v_add_f32",
+                           "v_mul_f32", "v_xor_b32", "v_rcp_f32"};
     const int cfg[4][2] = {{256, 1}, {512, 1}, {1024, 1}, {1024, 2}};  // 1, 2, 4, 8 waves per SIMD
-    double ghz = 0;
-    std::printf("{\"cus\": %d, \"memtime_ticks_per_wave64_instruction_per_simd\": {", cus);
-    for (int k = 0; k < 6; ++k) {
+    double ghz = 0, fma64_tflops = 0;
+    std::printf("{\"cus\": %d, \"cycles_per_wave64_instruction_per_simd\": {", cus);
+    for (int k = 0; k < 9; ++k) {
         std::printf("%s\"%s\": {", k ? ", " : "", names[k]);
         for (int c = 0; c < 4; ++c) {
             double r = 0;
@@ -119,11 +126,19 @@ int main() {
                 case 3: r = measure<3, double>(cus, th, bp, &ghz); break;
                 case 4: r = measure<4, double>(cus, th, bp, &ghz); break;
                 case 5: r = measure<5, float>(cus, th, bp, &ghz); break;
+                case 6: r = measure<6, float>(cus, th, bp, &ghz); break;
+                case 7: r = measure<7, float>(cus, th, bp, &ghz); break;
+                case 8: r = measure<8, float>(cus, th, bp, &ghz); break;
+            }
+            if (k == 3 && c == 3) {  // v_fma_f64 at 8 waves: the wall-clock rate
+                const double insts = static_cast<double>(cus) * bp * (th / 64) * kIters * kUnroll;
+                std::fprintf(stderr, "v_fma_f64 8 waves: %.3f ms, %.1f TFLOP/s f64\n", g_last_ms, insts * 64 * 2 / (g_last_ms * 1e-3) / 1e12);
+                fma64_tflops = insts * 64 * 2 / (g_last_ms * 1e-3) / 1e12;
             }
             std::printf("%s\"%d_waves\": %.3f", c ? ", " : "", th / 64 * bp / 4, r);
         }
         std::printf("}");
     }
-    std::printf("}, \"memtime_ghz_vs_memrealtime\": %.3f}\n", ghz);
+    std::printf("}, \"shader_clock_ghz\": %.3f, \"v_fma_f64_8_waves_wall_tflops\": %.1f}\n", ghz, fma64_tflops);
     return 0;
 }
