@@ -45,3 +45,46 @@ def test_glibc_pow_within_one_ulp_of_pow5_both_variants(fuzzer):
         assert r["undecided"] == 0, r
     # the two glibc variants give different results (the tunable took effect)
     assert fma["mismatches"] != sse2["mismatches"]
+
+
+def test_guard_flags_exactly_the_ambiguous_draws(tmp_path):
+    """schlick_undecided(u, r0, p) is true iff `u < r0 + (1 - r0) q` differs between q = pred(p)
+    and q = succ(p) (the branch a one-ulp different pow could flip): checked on draws at, just
+    below and just above the reflectance of random p, against the definition."""
+    src = tmp_path / "g.cpp"
+    src.write_text(r'''
+#include <cmath>
+#include <cstdio>
+#include <cstdint>
+#include "crt_schlick.h"
+int main() {
+    uint64_t s = 12345;
+    long bad = 0, flagged = 0, n = 0;
+    for (int i = 0; i < 2000000; ++i) {
+        s = s * 6364136223846793005ull + 1442695040888963407ull;
+        const double p = crt::pow5(static_cast<double>(s >> 11) * 0x1p-53);
+        const double r0 = 0.04 + 0.5 * static_cast<double>((s >> 7) & 0xffff) / 65536.0;
+        const double R = r0 + (1 - r0) * p;
+        const double us[5] = {R, std::nextafter(R, 0.0), std::nextafter(R, 2.0),
+                              r0 + (1 - r0) * crt::schlick_pred(p), r0 + (1 - r0) * crt::schlick_succ(p)};
+        for (double u : us) {
+            const bool a = u < r0 + (1 - r0) * crt::schlick_pred(p);
+            const bool b = u < r0 + (1 - r0) * crt::schlick_succ(p);
+            const bool want = a != b;
+            const bool got = crt::schlick_undecided(u, r0, p);
+            bad += want != got;
+            flagged += got;
+            ++n;
+        }
+    }
+    std::printf("%ld %ld %ld\n", n, flagged, bad);
+    return bad != 0;
+}
+''')
+    exe = tmp_path / "g"
+    subprocess.run(["g++", "-std=c++20", "-O2", "-ffp-contract=off", f"-I{ROOT / 'cpp_raytracer_amd' / 'csrc'}",
+                    str(src), "-o", str(exe)], check=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    n, flagged, bad = map(int, r.stdout.split())
+    assert r.returncode == 0 and bad == 0
+    assert flagged > 0  # the constructed draws do hit the ambiguous window
