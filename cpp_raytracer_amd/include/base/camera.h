@@ -131,6 +131,16 @@ class Camera {
         auto t0 = std::chrono::steady_clock::now();
         if (crt_render(scene, &resolved, devices, rgb.data(), &stats)) crt_api::die("Camera::render");
         auto ms = ms_diff(t0, std::chrono::steady_clock::now());
+        // parity guard (crt_render_guard): Dielectric branches a one-ulp different pow could flip
+        uint64_t undecided = 0;
+        for (int d = 0; d < devices; ++d) {
+            uint64_t n = 0;
+            if (crt_render_guard(scene, d, &n, 1) == 0) undecided += n;
+        }
+        if (undecided)
+            std::cerr << "Camera::render: " << undecided << " Dielectric reflect-or-refract decision(s) depend on "
+                      << "the last bit of pow(1 - cos, 5); the CPU reference's glibc may take the other branch there"
+                      << std::endl;
         std::cout << "Rendering " << image_w << " x " << image_h << " image: Finished in " << ms << "ms\n"
                   << std::endl;
         auto img = Image::with_dimensions(image_w, image_h);
