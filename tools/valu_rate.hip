@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <vector>
 
+typedef float F2 __attribute__((ext_vector_type(2)));
 constexpr int kIters = 4096;
 constexpr int kUnroll = 16;
 
@@ -25,6 +26,16 @@ constexpr int kUnroll = 16;
                  OP " %6, %6, %8, %9\n\t" OP " %7, %7, %8, %9"                                           \
                  : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7)      \
                  : "v"(b), "v"(c))
+#define CHAIN8_MASK(OP)                                                                                  \
+    asm volatile(OP " %0, %0, %8, %9\n\t" OP " %1, %1, %8, %9\n\t" OP " %2, %2, %8, %9\n\t"              \
+                 OP " %3, %3, %8, %9\n\t" OP " %4, %4, %8, %9\n\t" OP " %5, %5, %8, %9\n\t"              \
+                 OP " %6, %6, %8, %9\n\t" OP " %7, %7, %8, %9"                                           \
+                 : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7)      \
+                 : "v"(b), "s"(mask))
+#define CHAIN8_CMP(OP)                                                                                   \
+    asm volatile(OP " %0, %1, %9\n\t" OP " %0, %2, %9\n\t" OP " %0, %3, %9\n\t" OP " %0, %4, %9\n\t"     \
+                 OP " %0, %5, %9\n\t" OP " %0, %6, %9\n\t" OP " %0, %7, %9\n\t" OP " %0, %8, %9"         \
+                 : "=s"(mask) : "v"(a0), "v"(a1), "v"(a2), "v"(a3), "v"(a4), "v"(a5), "v"(a6), "v"(a7), "v"(b))
 #define CHAIN8_UN(OP)                                                                            \
     asm volatile(OP " %0, %0\n\t" OP " %1, %1\n\t" OP " %2, %2\n\t" OP " %3, %3\n\t"             \
                  OP " %4, %4\n\t" OP " %5, %5\n\t" OP " %6, %6\n\t" OP " %7, %7"                 \
@@ -32,6 +43,7 @@ constexpr int kUnroll = 16;
 
 template <int KIND, typename T>
 __global__ __launch_bounds__(1024) void rate_kernel(unsigned long long* cycles, unsigned long long* real, T* sink, T seed) {
+    unsigned long long mask = 0x5555555555555555ull;
     T a0 = seed, a1 = seed + 1, a2 = seed + 2, a3 = seed + 3, a4 = seed + 4, a5 = seed + 5, a6 = seed + 6,
       a7 = seed + 7, b = seed * T(0.5), c = seed * T(0.25);
     __syncthreads();
@@ -49,12 +61,25 @@ __global__ __launch_bounds__(1024) void rate_kernel(unsigned long long* cycles, 
             if constexpr (KIND == 6) CHAIN8("v_mul_f32");
             if constexpr (KIND == 7) CHAIN8("v_xor_b32");
             if constexpr (KIND == 8) CHAIN8_UN("v_rcp_f32");
+            if constexpr (KIND == 9) CHAIN8_FMA("v_pk_fma_f32");
+            if constexpr (KIND == 10) CHAIN8("v_pk_add_f32");
+            if constexpr (KIND == 11) CHAIN8("v_min_f32");
+            if constexpr (KIND == 12) CHAIN8_FMA("v_max3_f32");
+            if constexpr (KIND == 13) CHAIN8_MASK("v_cndmask_b32_e64");
+            if constexpr (KIND == 14) CHAIN8("v_min_i32");
+            if constexpr (KIND == 15) CHAIN8("v_max_u32");
+            if constexpr (KIND == 16) CHAIN8_FMA("v_med3_f32");
+            if constexpr (KIND == 17) CHAIN8_FMA("v_min3_i32");
+            if constexpr (KIND == 18) CHAIN8("v_min_f64");
+            if constexpr (KIND == 19) CHAIN8_CMP("v_cmp_lt_f32_e64");
+            if constexpr (KIND == 20) CHAIN8_FMA("v_bfe_u32");
+            if constexpr (KIND == 21) CHAIN8_FMA("v_lshl_or_b32");
         }
     }
     const unsigned long long t1 = __builtin_amdgcn_s_memtime();
     const unsigned long long r1 = __builtin_amdgcn_s_memrealtime();
     // every lane writes (vector stores): the chains stay live
-    sink[blockIdx.x * blockDim.x + threadIdx.x] = a0 + a1 + a2 + a3 + a4 + a5 + a6 + a7;
+    sink[blockIdx.x * blockDim.x + threadIdx.x] = a0 + a1 + a2 + a3 + a4 + a5 + a6 + a7 + T(static_cast<float>(mask & 1));
     if ((threadIdx.x & 63) == 0) {
         cycles[(blockIdx.x * blockDim.x + threadIdx.x) >> 6] = t1 - t0;
         real[(blockIdx.x * blockDim.x + threadIdx.x) >> 6] = r1 - r0;  // 100 MHz
@@ -110,11 +135,13 @@ int main() {
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0) != hipSuccess) return 1;
     const char* names[] = {"v_fma_f32", "v_add_f64", "v_mul_f64", "v_fma_f64", "v_rcp_f64", "v_add_f32",
-                           "v_mul_f32", "v_xor_b32", "v_rcp_f32"};
+                           "v_mul_f32", "v_xor_b32", "v_rcp_f32", "v_pk_fma_f32", "v_pk_add_f32", "v_min_f32",
+                           "v_max3_f32", "v_cndmask_b32", "v_min_i32", "v_max_u32", "v_med3_f32", "v_min3_i32",
+                           "v_min_f64", "v_cmp_lt_f32", "v_bfe_u32", "v_lshl_or_b32"};
     const int cfg[4][2] = {{256, 1}, {512, 1}, {1024, 1}, {1024, 2}};  // 1, 2, 4, 8 waves per SIMD
     double ghz = 0, fma64_tflops = 0;
     std::printf("{\"cus\": %d, \"cycles_per_wave64_instruction_per_simd\": {", cus);
-    for (int k = 0; k < 9; ++k) {
+    for (int k = 0; k < 22; ++k) {
         std::printf("%s\"%s\": {", k ? ", " : "", names[k]);
         for (int c = 0; c < 4; ++c) {
             double r = 0;
@@ -129,6 +156,19 @@ int main() {
                 case 6: r = measure<6, float>(cus, th, bp, &ghz); break;
                 case 7: r = measure<7, float>(cus, th, bp, &ghz); break;
                 case 8: r = measure<8, float>(cus, th, bp, &ghz); break;
+                case 9: r = measure<9, F2>(cus, th, bp, &ghz); break;
+                case 10: r = measure<10, F2>(cus, th, bp, &ghz); break;
+                case 11: r = measure<11, float>(cus, th, bp, &ghz); break;
+                case 12: r = measure<12, float>(cus, th, bp, &ghz); break;
+                case 13: r = measure<13, float>(cus, th, bp, &ghz); break;
+                case 14: r = measure<14, float>(cus, th, bp, &ghz); break;
+                case 15: r = measure<15, float>(cus, th, bp, &ghz); break;
+                case 16: r = measure<16, float>(cus, th, bp, &ghz); break;
+                case 17: r = measure<17, float>(cus, th, bp, &ghz); break;
+                case 18: r = measure<18, double>(cus, th, bp, &ghz); break;
+                case 19: r = measure<19, float>(cus, th, bp, &ghz); break;
+                case 20: r = measure<20, float>(cus, th, bp, &ghz); break;
+                case 21: r = measure<21, float>(cus, th, bp, &ghz); break;
             }
             if (k == 3 && c == 3) {  // v_fma_f64 at 8 waves: the wall-clock rate
                 const double insts = static_cast<double>(cus) * bp * (th / 64) * kIters * kUnroll;
