@@ -15,10 +15,12 @@ N GPUs are visible; under a launcher (WORLD_SIZE set) it is one rank.
 Prints ONE JSON line on rank 0 (see the repo contract), with
   roofline:     the resource that binds the render kernel. The scene is LDS/L2-resident and the
                 kernel moves ~7 GB per launch to/from HBM (~1% of peak), so the bound is VALU
-                issue: bound "valu", frac = VALU issue cycles / SIMD cycles of the timed kernel
-                from the rocprofv3 PMC passes of this exact build (profiles/pmc_latest.json: the
-                instruction-class counters at the per-instruction costs tools/valu_rate.hip
-                measured on the MI355X), lane_util = active lanes per VALU instruction. The HBM figures are reported beside it, labelled: `hbm.algorithmic`
+                issue: bound "valu", frac = the share of SIMD cycles the VALU issue port is busy
+                in the timed kernel, from the rocprofv3 PMC passes of this exact build
+                (profiles/pmc_latest.json: 4 x (SQ_ACTIVE_INST_VALU - SQ_ACTIVE_INST_VALU2) /
+                SIMD cycles, i.e. VALU issue quad-cycles net of gfx950 dual issue; the older
+                instruction-class model is kept beside it), lane_util = active lanes per VALU
+                instruction. The HBM figures are reported beside it, labelled: `hbm.algorithmic`
                 = SURVEY 8d bytes (56 B per BVH node visited, 36 B per sphere test, 124 B per
                 parallelogram test, 24 B per pixel written; visit counts from an untimed
                 instrumented pass) / kernel time — bytes the path touches, almost all served by
@@ -314,16 +316,19 @@ def main() -> int:
         "bound": "valu",
         "achieved": round(issue, 4) if issue is not None else None,
         "peak": 1.0,
-        "unit": "VALU issue cycles per SIMD cycle",
+        "unit": "VALU issue-busy cycles per SIMD cycle",
         "frac": round(issue, 4) if issue is not None else None,
         "traffic": traffic,
         "lane_util": round(pmc_data["valu_lane_utilization"], 4) if pmc_data and "valu_lane_utilization" in pmc_data else None,
         "valu_basis": (pmc_data.get("valu_issue_basis") if pmc_data else None),
         "valu_frac_simple_model": (round(pmc_data["valu_issue_frac_model"], 4)
                                    if pmc_data and "valu_issue_frac_model" in pmc_data else None),
-        "valu_costs": "SIMD cycles per wave64 instruction measured on the MI355X by tools/valu_rate.hip: f32 / int32 2, "
-                      "f64 4, f32 transcendental 8, f64 transcendental 16; over 32 x SQ_BUSY_CYCLES (1024 SIMDs), "
-                      "cross-checked against GRBM_GUI_ACTIVE",
+        "valu_frac_class_model": (round(pmc_data["valu_issue_frac_class_model"], 4)
+                                  if pmc_data and "valu_issue_frac_class_model" in pmc_data else None),
+        "valu_dual_issue_share": (round(pmc_data["valu_dual_issue_share"], 4)
+                                  if pmc_data and "valu_dual_issue_share" in pmc_data else None),
+        "valu_costs": "SIMD cycles = 32 x SQ_BUSY_CYCLES (1024 SIMDs), cross-checked against GRBM_GUI_ACTIVE; "
+                      "class model: per-instruction costs measured by tools/valu_rate.hip",
         "pmc_source": pmc_src,
         "kernel_ms": round(kernel_ms, 3),
         "hbm": {

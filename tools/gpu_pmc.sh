@@ -2,7 +2,7 @@
 # PMC passes of one bench workload: one rocprofv3 --pmc run per counter group (no --pmc mixed with
 # tracing options; at most 8 SQ / 4 TCC / 2 GRBM per pass), each under its own time limit, then
 # tools/pmc_summary.py -> <outdir>/summary.json.
-#   tools/gpu_pmc.sh <outdir under gpurun_out> [bench.py args]
+#   tools/gpu_pmc.sh <outdir under gpurun_out> [bench.py args]   (PASSES="3 6": those passes only)
 # Counters absent from `rocprofv3 -L` on this box are dropped from their pass.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -20,10 +20,14 @@ P2=$(pick WRITE_SIZE TCC_HIT_sum TCC_MISS_sum)
 P3=$(pick SQ_INSTS_VALU SQ_BUSY_CYCLES SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU)
 P4=$(pick SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVES SQ_LDS_BANK_CONFLICT)
 P5=$(pick SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_CVT SQ_INSTS_VALU)
+# issue slots: VALU quad-cycles per wave, the quad-cycles two VALU instructions issued together
+# (gfx950 dual issue), and the other issue units
+P6=$(pick SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VALU2 SQ_BUSY_CYCLES SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_MISC SQ_ACTIVE_INST_VMEM SQ_INST_CYCLES_SALU GRBM_GUI_ACTIVE)
 i=0
-for grp in "$P1" "$P2" "$P3" "$P4" "$P5"; do
+for grp in "$P1" "$P2" "$P3" "$P4" "$P5" "$P6"; do
   i=$((i+1))
   [ -n "$grp" ] || continue
+  case " ${PASSES:-1 2 3 4 5 6} " in *" $i "*) ;; *) continue ;; esac
   timeout -s KILL 240 rocprofv3 --pmc $grp --kernel-trace --output-format csv -d "$OUT/p$i" -o run -- python3 "$R/bench.py" $ARGS > "$OUT/bench_p$i.json" 2> "$OUT/bench_p$i.err" || { echo "pmc pass $i ($grp) failed"; tail -5 "$OUT/bench_p$i.err"; exit 1; }
   echo "pmc pass $i ok: $grp"
 done

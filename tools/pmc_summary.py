@@ -21,6 +21,14 @@ the effective clock GRBM_GUI_ACTIVE / 8 / kernel time. Issue cycles two ways:
                             transcendental 16.16 (16). The summary uses the nominal values the
                             measurement confirms; CVT and int64 count as f64-class (4), every
                             other VALU instruction (moves, selects, compares, packed f32) as 2.
+  valu_busy_frac            (when pass 6 ran; then also valu_issue_frac) model-free: the quad-cycles
+                            the waves issue VALU work (SQ_ACTIVE_INST_VALU, summed over waves)
+                            less the quad-cycles two waves issued together (SQ_ACTIVE_INST_VALU2,
+                            gfx950 dual issue), x 4, over the SIMD cycles. The class model above
+                            undercounts: most "other" instructions (v_cndmask, v_cmp, v_min / max,
+                            v_bfe, packed f32, conversions) take a full quad-cycle (4.1-4.3 cycles,
+                            profiles/r03_v3/valu_rate_ext.json); only f32 add / mul / fma, v_mov,
+                            v_add_u32, v_xor pair up (2.3).
 
 usage: python tools/pmc_summary.py <pmc dir> <out.json> [workload]
 The workload key defaults to config.workload of <dir>/bench_p1.json (the bench line of pass 1);
@@ -96,6 +104,25 @@ def main():
         res["valu_issue_frac"] = res.get("valu_issue_frac_measured", res["valu_issue_frac_model"])
         res["valu_issue_basis"] = ("per-class costs measured by tools/valu_rate.hip" if "valu_issue_frac_measured" in res
                                    else "model: 2 cycles per wave64 instruction, 4 per f64")
+    if "SQ_ACTIVE_INST_VALU2" in avg and "SQ_ACTIVE_INST_VALU" in avg and "SQ_BUSY_CYCLES" in avg:
+        # counter-based, no cost model: SQ_ACTIVE_INST_VALU = quad-cycles each wave issues VALU work
+        # (summed over waves; 1 per instruction, 2 / 4 for f32 / f64 transcendentals),
+        # SQ_ACTIVE_INST_VALU2 = quad-cycles in which two waves' VALU instructions issued together
+        # (gfx950 dual issue, counted under both waves above): the SIMD's VALU issue port is busy
+        # 4 x (VALU - VALU2) of its cycles
+        simd = 32 * avg["SQ_BUSY_CYCLES"]
+        res["simd_cycles"] = simd
+        res["valu_busy_quads"] = avg["SQ_ACTIVE_INST_VALU"] - avg["SQ_ACTIVE_INST_VALU2"]
+        res["valu_busy_frac"] = 4 * res["valu_busy_quads"] / simd
+        res["valu_dual_issue_share"] = 2 * avg["SQ_ACTIVE_INST_VALU2"] / avg["SQ_ACTIVE_INST_VALU"]
+        for k in ("SCA", "LDS", "MISC", "VMEM"):
+            if f"SQ_ACTIVE_INST_{k}" in avg:
+                res[f"{k.lower()}_busy_frac"] = 4 * avg[f"SQ_ACTIVE_INST_{k}"] / simd
+        if "valu_issue_frac" in res:
+            res["valu_issue_frac_class_model"] = res["valu_issue_frac"]
+        res["valu_issue_frac"] = res["valu_busy_frac"]
+        res["valu_issue_basis"] = ("counters: 4 x (SQ_ACTIVE_INST_VALU - SQ_ACTIVE_INST_VALU2) / (32 x SQ_BUSY_CYCLES), "
+                                   "the SIMDs' VALU issue quad-cycles net of dual issue")
     if "GRBM_GUI_ACTIVE" in avg:
         res["simd_cycles_from_grbm"] = 1024 * avg["GRBM_GUI_ACTIVE"] / 8
         if durs:

@@ -36,6 +36,11 @@ constexpr int kUnroll = 16;
     asm volatile(OP " %0, %1, %9\n\t" OP " %0, %2, %9\n\t" OP " %0, %3, %9\n\t" OP " %0, %4, %9\n\t"     \
                  OP " %0, %5, %9\n\t" OP " %0, %6, %9\n\t" OP " %0, %7, %9\n\t" OP " %0, %8, %9"         \
                  : "=s"(mask) : "v"(a0), "v"(a1), "v"(a2), "v"(a3), "v"(a4), "v"(a5), "v"(a6), "v"(a7), "v"(b))
+#define CHAIN8_CVT(OP)                                                                           \
+    asm volatile(OP " %0, %8\n\t" OP " %1, %8\n\t" OP " %2, %8\n\t" OP " %3, %8\n\t"             \
+                 OP " %4, %8\n\t" OP " %5, %8\n\t" OP " %6, %8\n\t" OP " %7, %8"                 \
+                 : "=v"(a0), "=v"(a1), "=v"(a2), "=v"(a3), "=v"(a4), "=v"(a5), "=v"(a6), "=v"(a7)  \
+                 : "v"(ub))
 #define CHAIN8_UN(OP)                                                                            \
     asm volatile(OP " %0, %0\n\t" OP " %1, %1\n\t" OP " %2, %2\n\t" OP " %3, %3\n\t"             \
                  OP " %4, %4\n\t" OP " %5, %5\n\t" OP " %6, %6\n\t" OP " %7, %7"                 \
@@ -44,6 +49,7 @@ constexpr int kUnroll = 16;
 template <int KIND, typename T>
 __global__ __launch_bounds__(1024) void rate_kernel(unsigned long long* cycles, unsigned long long* real, T* sink, T seed) {
     unsigned long long mask = 0x5555555555555555ull;
+    unsigned ub = threadIdx.x * 7919u + 13u;
     T a0 = seed, a1 = seed + 1, a2 = seed + 2, a3 = seed + 3, a4 = seed + 4, a5 = seed + 5, a6 = seed + 6,
       a7 = seed + 7, b = seed * T(0.5), c = seed * T(0.25);
     __syncthreads();
@@ -74,6 +80,16 @@ __global__ __launch_bounds__(1024) void rate_kernel(unsigned long long* cycles, 
             if constexpr (KIND == 19) CHAIN8_CMP("v_cmp_lt_f32_e64");
             if constexpr (KIND == 20) CHAIN8_FMA("v_bfe_u32");
             if constexpr (KIND == 21) CHAIN8_FMA("v_lshl_or_b32");
+            if constexpr (KIND == 22) CHAIN8("v_mul_lo_u32");
+            if constexpr (KIND == 23) CHAIN8("v_mul_hi_u32");
+            if constexpr (KIND == 24) CHAIN8_FMA("v_mad_u32_u24");
+            if constexpr (KIND == 25) CHAIN8_CVT("v_cvt_f32_u32");
+            if constexpr (KIND == 26) CHAIN8_CVT("v_cvt_f64_u32");
+            if constexpr (KIND == 27) CHAIN8_UN("v_rsq_f64");
+            if constexpr (KIND == 28) CHAIN8_UN("v_sqrt_f64");
+            if constexpr (KIND == 29) CHAIN8_CMP("v_cmp_lt_f64_e64");
+            if constexpr (KIND == 30) CHAIN8_UN("v_mov_b32");
+            if constexpr (KIND == 31) CHAIN8("v_add_u32");
         }
     }
     const unsigned long long t1 = __builtin_amdgcn_s_memtime();
@@ -137,11 +153,14 @@ int main() {
     const char* names[] = {"v_fma_f32", "v_add_f64", "v_mul_f64", "v_fma_f64", "v_rcp_f64", "v_add_f32",
                            "v_mul_f32", "v_xor_b32", "v_rcp_f32", "v_pk_fma_f32", "v_pk_add_f32", "v_min_f32",
                            "v_max3_f32", "v_cndmask_b32", "v_min_i32", "v_max_u32", "v_med3_f32", "v_min3_i32",
-                           "v_min_f64", "v_cmp_lt_f32", "v_bfe_u32", "v_lshl_or_b32"};
+                           "v_min_f64", "v_cmp_lt_f32", "v_bfe_u32", "v_lshl_or_b32", "v_mul_lo_u32",
+                           "v_mul_hi_u32", "v_mad_u32_u24", "v_cvt_f32_u32", "v_cvt_f64_u32", "v_rsq_f64",
+                           "v_sqrt_f64", "v_cmp_lt_f64", "v_mov_b32", "v_add_u32"};
+    constexpr int kKinds = sizeof(names) / sizeof(names[0]);
     const int cfg[4][2] = {{256, 1}, {512, 1}, {1024, 1}, {1024, 2}};  // 1, 2, 4, 8 waves per SIMD
     double ghz = 0, fma64_tflops = 0;
     std::printf("{\"cus\": %d, \"cycles_per_wave64_instruction_per_simd\": {", cus);
-    for (int k = 0; k < 22; ++k) {
+    for (int k = 0; k < kKinds; ++k) {
         std::printf("%s\"%s\": {", k ? ", " : "", names[k]);
         for (int c = 0; c < 4; ++c) {
             double r = 0;
@@ -169,6 +188,16 @@ int main() {
                 case 19: r = measure<19, float>(cus, th, bp, &ghz); break;
                 case 20: r = measure<20, float>(cus, th, bp, &ghz); break;
                 case 21: r = measure<21, float>(cus, th, bp, &ghz); break;
+                case 22: r = measure<22, float>(cus, th, bp, &ghz); break;
+                case 23: r = measure<23, float>(cus, th, bp, &ghz); break;
+                case 24: r = measure<24, float>(cus, th, bp, &ghz); break;
+                case 25: r = measure<25, float>(cus, th, bp, &ghz); break;
+                case 26: r = measure<26, double>(cus, th, bp, &ghz); break;
+                case 27: r = measure<27, double>(cus, th, bp, &ghz); break;
+                case 28: r = measure<28, double>(cus, th, bp, &ghz); break;
+                case 29: r = measure<29, double>(cus, th, bp, &ghz); break;
+                case 30: r = measure<30, float>(cus, th, bp, &ghz); break;
+                case 31: r = measure<31, float>(cus, th, bp, &ghz); break;
             }
             if (k == 3 && c == 3) {  // v_fma_f64 at 8 waves: the wall-clock rate
                 const double insts = static_cast<double>(cus) * bp * (th / 64) * kIters * kUnroll;
