@@ -2483,18 +2483,23 @@ static int launch_render(const crt_scene* s, int device, const crt_camera* cam, 
             W.tiles = W.tiles_x * W.tiles_y;
             const uint64_t blocks = std::max<uint64_t>(
                 1, std::min<uint64_t>(resident, (static_cast<uint64_t>(W.tiles) * W.chunks + kWavesPerBlock - 1) / kWavesPerBlock));
-            // Items: bulk items of K chunks for the first 8/9 of each tile's chunks, then the
+            // Items: bulk items of K chunks for the first part of each tile's chunks, then the
             // rest in one-chunk items at the end of the queue (CRT_TAIL_CHUNKS), so the grid
             // drains on small items; a wave's lanes cross from item to item without waiting
-            // either way. K keeps an item small against a wave's share of the band (a tile costs
-            // up to ~10x another): a 30th of the units per lane, at most 7 (config 2: 7 on one
-            // GPU, 3/1/1 for a rank's share at 2/4/8 GPUs; no tail items with K = 1). Measured on
-            // config 2, one GPU (Msamples/s): K = 1 5127, 7 5273, 14 4828, 28 4025; a rank's
-            // share at 4 / 8 GPUs took 24.8 / 14.1 ms with K = 1, 26.1 / 19.4 with K = 2 / 7
-            // (CRT_ITEM_CHUNKS, CRT_TAIL_CHUNKS override).
+            // either way. Large items keep a wave's lanes on one tile (coherent rays: config 2 on
+            // one GPU takes 72.5 ms with K = 7, 77.1 with K = 1), small ones balance the drain
+            // against a ~10x spread of tile costs. With p = (tile, chunk) pairs per wave: K =
+            // min(7, p / 15) for p >= 60, else 1 (no tail), and the tail takes max(1/9, 30 / p) of
+            // the chunks. Config 2, the slowest rank's share (tools/item_sweep.py,
+            // profiles/r03_schedule): N = 2 (p = 183) 36.9 -> 36.7 ms, N = 4 (p = 92) 19.7 -> 19.0
+            // against the earlier K = p / 30 with a 1/9 tail; N = 1 (7, 13 of 125 chunks) and
+            // N = 8 (K = 1) unchanged. (CRT_ITEM_CHUNKS, CRT_TAIL_CHUNKS override.)
             const uint64_t per_lane = static_cast<uint64_t>(W.tiles) * W.chunks / (blocks * kWavesPerBlock);
-            W.item_chunks = std::max<uint32_t>(1, knob("CRT_ITEM_CHUNKS", static_cast<uint32_t>(std::min<uint64_t>(7, std::max<uint64_t>(1, per_lane / 30)))));
-            const uint32_t tail_want = std::min(W.chunks, knob("CRT_TAIL_CHUNKS", W.item_chunks > 1 ? W.chunks / 9 : 0));
+            const uint32_t k_auto = per_lane >= 60 ? static_cast<uint32_t>(std::min<uint64_t>(7, per_lane / 15)) : 1u;
+            W.item_chunks = std::max<uint32_t>(1, knob("CRT_ITEM_CHUNKS", k_auto));
+            const uint32_t tail_auto = static_cast<uint32_t>(std::max<uint64_t>(
+                W.chunks / 9, std::min<uint64_t>(W.chunks, static_cast<uint64_t>(W.chunks) * 30 / std::max<uint64_t>(1, per_lane))));
+            const uint32_t tail_want = std::min(W.chunks, knob("CRT_TAIL_CHUNKS", W.item_chunks > 1 ? tail_auto : 0));
             W.groups = (W.chunks - tail_want) / W.item_chunks;
             W.bulk_chunks = W.groups * W.item_chunks;
             W.tail_chunks = W.chunks - W.bulk_chunks;
