@@ -129,6 +129,10 @@ def main():
             res["effective_clock_ghz"] = avg["GRBM_GUI_ACTIVE"] / 8 / res["kernel_ns_under_pmc"]
     if "SQ_THREAD_CYCLES_VALU" in avg and "SQ_ACTIVE_INST_VALU" in avg:
         res["valu_lane_utilization"] = avg["SQ_THREAD_CYCLES_VALU"] / (64 * avg["SQ_ACTIVE_INST_VALU"])
+    if "SQ_WAVE_CYCLES" in avg and "simd_cycles" in res:
+        # resident waves per SIMD, averaged over the kernel (SQ_WAVE_CYCLES counts quad-cycles);
+        # a block that no longer fits in LDS shows here as one wave fewer
+        res["avg_waves_per_simd"] = 4 * avg["SQ_WAVE_CYCLES"] / res["simd_cycles"]
     if "SQ_WAVE_CYCLES" in avg:
         for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
             if k in avg:
