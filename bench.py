@@ -327,6 +327,8 @@ def main() -> int:
                                   if pmc_data and "valu_issue_frac_class_model" in pmc_data else None),
         "valu_dual_issue_share": (round(pmc_data["valu_dual_issue_share"], 4)
                                   if pmc_data and "valu_dual_issue_share" in pmc_data else None),
+        "waves_per_simd": (round(pmc_data["avg_waves_per_simd"], 2)
+                           if pmc_data and "avg_waves_per_simd" in pmc_data else None),
         "valu_costs": "SIMD cycles = 32 x SQ_BUSY_CYCLES (1024 SIMDs), cross-checked against GRBM_GUI_ACTIVE; "
                       "class model: per-instruction costs measured by tools/valu_rate.hip",
         "pmc_source": pmc_src,
