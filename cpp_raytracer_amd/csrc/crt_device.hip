@@ -2489,13 +2489,14 @@ static int launch_render(const crt_scene* s, int device, const crt_camera* cam, 
             // either way. Large items keep a wave's lanes on one tile (coherent rays: config 2 on
             // one GPU takes 72.5 ms with K = 7, 77.1 with K = 1), small ones balance the drain
             // against a ~10x spread of tile costs. With p = (tile, chunk) pairs per wave: K =
-            // min(7, p / 15) for p >= 60, else 1 (no tail), and the tail takes max(1/9, 30 / p) of
-            // the chunks. Config 2, the slowest rank's share (tools/item_sweep.py,
-            // profiles/r03_schedule): N = 2 (p = 183) 36.9 -> 36.7 ms, N = 4 (p = 92) 19.7 -> 19.0
-            // against the earlier K = p / 30 with a 1/9 tail; N = 1 (7, 13 of 125 chunks) and
-            // N = 8 (K = 1) unchanged. (CRT_ITEM_CHUNKS, CRT_TAIL_CHUNKS override.)
+            // min(7, p / 15) for p >= 60, else 3, and the tail takes max(1/9, 30 / p) of the
+            // chunks (all of them for p <= 30). Config 2, the slowest rank's share
+            // (tools/item_sweep.py, tools/grid_sweep.py, profiles/r03_schedule): N = 2 (p = 183)
+            // 36.9 -> 36.7 ms, N = 4 (p = 92) 19.7 -> 19.0, N = 8 (p = 46, K = 3 with an 81-chunk
+            // tail) 10.34-10.49 -> 10.17-10.31 against the earlier K = p / 30 with a 1/9 tail;
+            // N = 1 (7, 13 of 125 chunks) unchanged. (CRT_ITEM_CHUNKS, CRT_TAIL_CHUNKS override.)
             const uint64_t per_lane = static_cast<uint64_t>(W.tiles) * W.chunks / (blocks * kWavesPerBlock);
-            const uint32_t k_auto = per_lane >= 60 ? static_cast<uint32_t>(std::min<uint64_t>(7, per_lane / 15)) : 1u;
+            const uint32_t k_auto = per_lane >= 60 ? static_cast<uint32_t>(std::min<uint64_t>(7, per_lane / 15)) : 3u;
             W.item_chunks = std::max<uint32_t>(1, knob("CRT_ITEM_CHUNKS", k_auto));
             const uint32_t tail_auto = static_cast<uint32_t>(std::max<uint64_t>(
                 W.chunks / 9, std::min<uint64_t>(W.chunks, static_cast<uint64_t>(W.chunks) * 30 / std::max<uint64_t>(1, per_lane))));
