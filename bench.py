@@ -27,9 +27,10 @@ Prints ONE JSON line on rank 0 (see the repo contract), with
                 LDS and L1/L2, so its "fraction" may exceed 1 — and `hbm.measured` = PMC HBM bytes
                 (FETCH_SIZE x2 + WRITE_SIZE) / kernel time against the 8 TB/s peak.
   cpu_baseline: the reference's own Camera::render (oracle/_ref, built from the reference
-                sources) on the host, median of 3 runs of a bounded sample of the same frame
-                (fewer spp), threads = the CPUs this process may use (OMP_NUM_THREADS when set:
-                the GPU box's share for one GPU), CPU model and host CPU count reported.
+                sources) on the host, as BASELINE.md §3 specifies: the same frame (config 2
+                whole, 500 spp), threads = every CPU this process may use, median of 3 runs; CPU
+                model and host CPU count reported, and a secondary one-run figure on the GPU's CPU
+                share (OMP_NUM_THREADS) beside it.
 """
 from __future__ import annotations
 
@@ -113,57 +114,84 @@ def parse():
     ap.add_argument("--spp", type=int, default=500)
     ap.add_argument("--depth", type=int, default=50)
     ap.add_argument("--base-seed", type=int, default=2024)
-    ap.add_argument("--cpu-spp", type=int, default=250, help="spp of the CPU-baseline sample (the same frame)")
+    ap.add_argument("--cpu-spp", type=int, default=0,
+                    help="spp of the CPU-baseline frame (0 = the benchmarked spp: BASELINE.md §3 runs config 2 whole)")
     ap.add_argument("--cpu-runs", type=int, default=3, help="CPU-baseline runs (the median is reported)")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = OMP_NUM_THREADS, else the usable CPUs")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="0 = every CPU this process may use (BASELINE.md §3: OMP_NUM_THREADS=nproc)")
+    ap.add_argument("--cpu-share-spp", type=int, default=250,
+                    help="spp of the secondary one-run figure on the GPU's CPU share (OMP_NUM_THREADS); 0 = skip")
     ap.add_argument("--launch-check", action="store_true",
                     help="ranks only join the process group and report (tests the N-rank launch on CPU)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dump-frame", default="", help="save every rank's last assembled frame to PATH.rank<r>.npy")
     ap.add_argument("--pmc-json", default=str(ROOT / "profiles" / "pmc_latest.json"))
     return ap.parse_args()
 
 
 def cpu_baseline(args, scene_data, log) -> dict | None:
-    """Reference Camera::render on the host, on a bounded sample of the same workload."""
+    """Reference Camera::render on the host, as BASELINE.md §3 specifies: the same frame (config 2
+    whole by default: 1200x800, 500 spp), OpenMP over every CPU this process may use, median of
+    --cpu-runs runs. A secondary one-run figure on the GPU's CPU share (OMP_NUM_THREADS, 16 on the
+    GPU box) at --cpu-share-spp is reported beside it, labelled."""
     import statistics
     import cpp_raytracer_amd as crt
     from cpp_raytracer_amd import camera_with
     model, host_cpus, usable = cpu_info()
-    threads = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or usable
+    threads = args.cpu_threads or usable
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
     ref = ROOT / "oracle" / "_ref" / "ref_driver"
     runs = max(1, args.cpu_runs)
-    sample = (f"{args.scene} seed {args.seed}, {args.width}x{args.height}, {args.cpu_spp} spp, depth {args.depth}; "
-              f"median of {runs} runs")
+    spp = args.cpu_spp or args.spp
     host = {"cpu_model": model, "host_cpus": host_cpus, "usable_cpus": usable}
-    d = crt.SceneData(scene_data.materials, scene_data.objects,
-                      camera_with(scene_data.camera, image_w=args.width, image_h=args.height,
-                                  samples_per_pixel=args.cpu_spp, max_depth=args.depth))
+
+    def frame(n_spp):
+        return crt.SceneData(scene_data.materials, scene_data.objects,
+                             camera_with(scene_data.camera, image_w=args.width, image_h=args.height,
+                                         samples_per_pixel=n_spp, max_depth=args.depth))
+
+    def desc(n_spp, n_runs):
+        return (f"{args.scene} seed {args.seed}, {args.width}x{args.height}, {n_spp} spp, depth {args.depth}"
+                + (f"; median of {n_runs} runs" if n_runs > 1 else "; one run"))
+
     with tempfile.TemporaryDirectory() as td:
-        p = Path(td) / "scene.crts"
-        d.save(p)
+        def ref_rates(n_spp, n_threads, n_runs):
+            p = Path(td) / f"scene_{n_spp}.crts"
+            if not p.exists():
+                frame(n_spp).save(p)
+            rates = []
+            for _ in range(n_runs):
+                r = subprocess.run([str(ref), "time", str(p), str(n_threads)], capture_output=True, text=True,
+                                   timeout=900, check=True)
+                j = json.loads(r.stdout.strip().splitlines()[-1])
+                rates.append(j["samples"] / j["seconds"] / 1e6)
+            return rates
+
         if ref.exists():
             try:
-                rates = []
-                for _ in range(runs):
-                    r = subprocess.run([str(ref), "time", str(p), str(threads)], capture_output=True, text=True,
-                                       timeout=600, check=True)
-                    j = json.loads(r.stdout.strip().splitlines()[-1])
-                    rates.append(j["samples"] / j["seconds"] / 1e6)
-                return {"value": round(statistics.median(rates), 4), "unit": "Msamples/s", "cores": threads,
-                        "kind": "reference", "runs": [round(x, 4) for x in rates], **host,
-                        "sample": sample + " (reference Camera::render, OpenMP, own per-thread RNG)"}
+                rates = ref_rates(spp, threads, runs)
+                out = {"value": round(statistics.median(rates), 4), "unit": "Msamples/s", "cores": threads,
+                       "kind": "reference", "runs": [round(x, 4) for x in rates], **host,
+                       "sample": desc(spp, runs) + " (reference Camera::render, OpenMP, own per-thread RNG)"}
+                if share and share != threads and args.cpu_share_spp:
+                    r2 = ref_rates(args.cpu_share_spp, share, 1)
+                    out["gpu_cpu_share"] = {"value": round(r2[0], 4), "unit": "Msamples/s", "cores": share,
+                                            "sample": desc(args.cpu_share_spp, 1) + " on OMP_NUM_THREADS "
+                                            "(the GPU box's CPU share for one GPU); secondary, not the baseline"}
+                return out
             except Exception as e:  # pragma: no cover - reported, not fatal
                 log(f"reference CPU baseline failed: {e}")
         try:
             sys.path.insert(0, str(ROOT / "oracle"))
             import crt_oracle_py as orc
+            d = frame(spp)
             rates = []
             for _ in range(runs):
                 secs, n = orc.time_render(d, threads, args.base_seed)
                 rates.append(n / secs / 1e6)
             return {"value": round(statistics.median(rates), 4), "unit": "Msamples/s", "cores": threads,
                     "kind": "port", "runs": [round(x, 4) for x in rates], **host,
-                    "sample": sample + " (oracle C restatement, OpenMP)"}
+                    "sample": desc(spp, runs) + " (oracle C restatement, OpenMP)"}
         except Exception as e:  # pragma: no cover
             log(f"port CPU baseline failed: {e}")
     return None
@@ -235,11 +263,18 @@ def main() -> int:
     log(f"scene {args.scene}: {info.num_primitives} prims, {info.num_nodes} nodes, depth {info.depth}, "
         f"BVH build {info.build_ms:.1f} ms, setup {time.time() - t0:.1f} s")
 
-    frames = [torch.zeros(h, w, 3, dtype=torch.float64, device="cuda") for _ in range(2 if distributed else 1)]
     gather = TileGather(h, w, world, rank, "cuda", row_block=rb)
+    # N > 1: each rank renders its rows only, packed in order into a tile of its share
+    # (CRT_TILING_PACKED), which is also the all-gather's input: no full-frame buffer per rank
+    if distributed:
+        tiling = Tiling(rb, world, rank, 1)
+        frames = [gather.new_tile() for _ in range(2)]
+    else:
+        frames = [torch.zeros(h, w, 3, dtype=torch.float64, device="cuda")]
     stream = torch.cuda.current_stream()
     side = torch.cuda.Stream() if distributed else None
     gathered = [None] * len(frames)  # per frame buffer: event after its last gather
+    assembled = [None]  # the last assembled frame (--dump-frame)
 
     def step(i, ev=None):
         # N > 1: frame i's tiles are all-gathered (RCCL over xGMI) on a side stream while frame
@@ -259,10 +294,12 @@ def main() -> int:
             rendered.record(stream)
             with torch.cuda.stream(side):
                 side.wait_event(rendered)
-                gather.gather(buf)
+                assembled[0] = gather.gather_packed(buf)
                 done = torch.cuda.Event()
                 done.record(side)
             gathered[k] = done
+        else:
+            assembled[0] = buf
 
     for i in range(args.warmup):
         step(i)
@@ -280,6 +317,9 @@ def main() -> int:
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t_start
     kernel_ms = sum(a.elapsed_time(b) for a, b in evs) / max(1, args.steps)
+    if args.dump_frame:  # every rank's last assembled frame (tests: equal to the 1-rank frame)
+        import numpy as np
+        np.save(f"{args.dump_frame}.rank{rank}.npy", assembled[0].cpu().numpy())
     if distributed:
         t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

@@ -209,6 +209,15 @@ class GpuScene:
               "crt_render")
         return out, st
 
+    def render_ppm(self, cam: Camera, num_devices: int = 1) -> tuple[np.ndarray, RenderStats]:
+        """Blocking whole-frame render fused with Image::send_as_ppm's integers (crt_render_ppm:
+        each device tone-maps its rows to 8-bit values before the gather): (h, w, 3) int32."""
+        out = np.empty((cam.image_h, cam.image_w, 3), np.int32)
+        st = RenderStats()
+        check(lib().crt_render_ppm(self._h, C.byref(cam), num_devices, out.ctypes.data, C.byref(st)),
+              "crt_render_ppm")
+        return out, st
+
     def guard(self, device: int = 0, reset: bool = False) -> int:
         """Dielectric decisions since upload (or the last reset) that a one-ulp different
         pow(1 - cos, 5) could have flipped (crt_render_guard; 0 = every branch as the reference's)."""

@@ -55,7 +55,7 @@ class Camera(C.Structure):
 
 class Tiling(C.Structure):
     _fields_ = [("row_block", C.c_uint32), ("tile_count", C.c_uint32),
-                ("tile_index", C.c_uint32), ("reserved", C.c_uint32)]
+                ("tile_index", C.c_uint32), ("flags", C.c_uint32)]
 
 
 class SceneInfo(C.Structure):
@@ -120,6 +120,7 @@ EXPORTS = {
     "crt_render_async": (C.c_int, [C.c_void_p, C.c_int, P(Camera), P(Tiling), C.c_void_p, C.c_void_p]),
     "crt_render_count": (C.c_int, [C.c_void_p, C.c_int, P(Camera), P(Tiling), P(RenderStats)]),
     "crt_render": (C.c_int, [C.c_void_p, P(Camera), C.c_int, C.c_void_p, P(RenderStats)]),
+    "crt_render_ppm": (C.c_int, [C.c_void_p, P(Camera), C.c_int, C.c_void_p, P(RenderStats)]),
     "crt_closest_hits": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t, C.c_double, C.c_double,
                                    C.c_void_p]),
     "crt_ppm_values": (C.c_int, [C.c_int, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p]),

@@ -722,6 +722,15 @@ int device_build_bvh(crt_scene* s, uint32_t num_buckets, uint32_t max_leaf, int 
     std::vector<TNode> tn;
     std::vector<uint32_t> order(n);
     uint32_t nnodes = 0;
+    const bool dbg = std::getenv("CRT_DEBUG_BUILD") != nullptr;
+    auto tp = std::chrono::steady_clock::now();
+    auto phase = [&](const char* what) {  // CRT_DEBUG_BUILD: where the build's time goes
+        if (!dbg) return;
+        (void)hipDeviceSynchronize();
+        const auto now = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "bvh phase %-10s %8.3f ms\n", what, std::chrono::duration<double, std::milli>(now - tp).count());
+        tp = now;
+    };
     {
         for (size_t i = 0; i < n; ++i) order[i] = static_cast<uint32_t>(i);
         BV_TRY(hipMalloc(&d_pb, n * 6 * sizeof(double)));
@@ -742,6 +751,7 @@ int device_build_bvh(crt_scene* s, uint32_t num_buckets, uint32_t max_leaf, int 
         BV_TRY(hipMalloc(&d_chunk_red, max_chunks * 12 * sizeof(double)));
         BV_TRY(hipMalloc(&d_bn, max_big * 3 * kMaxBuckets * sizeof(unsigned int)));
         BV_TRY(hipMalloc(&d_bb, max_big * 3 * kMaxBuckets * 6 * sizeof(unsigned long long)));
+        phase("alloc");
         BV_TRY(hipMemcpy(d_pb, boxes.data(), n * 6 * sizeof(double), hipMemcpyHostToDevice));
         BV_TRY(hipMemcpy(d_pc, cents.data(), n * 3 * sizeof(double), hipMemcpyHostToDevice));
         BV_TRY(hipMemcpy(d_order, order.data(), n * 4, hipMemcpyHostToDevice));
@@ -759,7 +769,7 @@ int device_build_bvh(crt_scene* s, uint32_t num_buckets, uint32_t max_leaf, int 
         }
         BV_TRY(hipMemcpy(d_ctr, ctr, sizeof ctr, hipMemcpyHostToDevice));
         const Params P{num_buckets, max_leaf};
-        const bool dbg = std::getenv("CRT_DEBUG_BUILD") != nullptr;
+        phase("upload");
         auto tl = std::chrono::steady_clock::now();
         int level = 0;
         std::vector<ChunkInfo> chunks;
@@ -813,11 +823,13 @@ int device_build_bvh(crt_scene* s, uint32_t num_buckets, uint32_t max_leaf, int 
             BV_TRY(hipMemcpy(d_ctr + 1, &ctr[1], 8, hipMemcpyHostToDevice));
             std::swap(d_ta, d_tb);
         }
+        phase("levels");
         nnodes = ctr[0];
         tn.resize(nnodes);
         BV_TRY(hipMemcpy(tn.data(), d_nodes, nnodes * sizeof(TNode), hipMemcpyDeviceToHost));
         BV_TRY(hipMemcpy(order.data(), d_order, n * 4, hipMemcpyDeviceToHost));
     }
+    phase("download");
     {
         // preorder numbering (bvh.h:468-550): children have larger build ids than parents
         std::vector<uint32_t> size(nnodes, 1), pre(nnodes, 0), lvl(nnodes, 1);
@@ -847,6 +859,7 @@ int device_build_bvh(crt_scene* s, uint32_t num_buckets, uint32_t max_leaf, int 
         }
         s->order = std::move(order);
     }
+    phase("preorder");
 done:
     (void)hipFree(d_pb);
     (void)hipFree(d_pc);

@@ -17,6 +17,7 @@
 #include <cstring>
 #include <limits>
 #include <string>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -47,19 +48,8 @@ constexpr int kBlock = CRT_BLOCK;
 #define CRT_TILE_W 16
 #endif
 constexpr uint32_t kTileW = CRT_TILE_W, kTileH = 64 / CRT_TILE_W;
-// the speculative walk's parked lanes leave the loop through the exec mask (1) or re-run its body
-// at their node (0)
-#ifndef CRT_SPEC_MASKED
-#define CRT_SPEC_MASKED 1
-#endif
-// the five-wave sphere-only instance keeps the lanes' pixel sums in LDS (render_kernel: kAccLds)
-#ifndef CRT_ACC_LDS
-#define CRT_ACC_LDS 1
-#endif
 // waves per SIMD of the W5 instances (the "five-wave" ones)
-#ifndef CRT_MANY_WAVES
-#define CRT_MANY_WAVES 5
-#endif
+constexpr int kManyWaves = 5;
 constexpr double kScale = 1 / static_cast<double>(4294967295u - 1);  // rand_util.h:110-112
 
 typedef double Dvec2 __attribute__((ext_vector_type(2)));
@@ -130,7 +120,10 @@ struct Work {
     uint32_t sentinel;      // the sentinel node's reference (byte offset into the f32 nodes)
     uint32_t lds_cam;       // LDS copy of the CamView (read where used: keeps it out of SGPRs)
     uint32_t lds_acc;       // five-wave instances: the lanes' pixel sums (3 x kBlock doubles)
-    uint32_t lds_cmp;       // candidate compaction (CRT_COMPACT_CAND): kCmpWaveBytes per wave
+    uint32_t packed;        // the output holds only the owned rows (CRT_TILING_PACKED)
+    // instrumented pass only (COUNT): walk speculatively like the timed kernel (CRT_COUNT_SPEC=1),
+    // count per-round lane numbers (CRT_ROUND_COUNTERS=1; their atomics shift the phase timings)
+    uint32_t count_spec, round_counters;
     uint32_t f32_ok;        // node bounds fit the f32 walk's error analysis (else f64 decides)
     uint32_t spheres_f32;   // sphere-only scene within the f32 filter's range (two-pass leaves)
     uint32_t quads_f32;     // parallelogram-only scene within its f32 filter's range (two-pass leaves)
@@ -231,13 +224,9 @@ __device__ __forceinline__ double sqrt_from_rsq(double x, double r) {
 // refraction) without the range scaling and special-case fix-ups of hipcc's IEEE expansions, in
 // the five-wave sphere-only kernel instances (FAST; config 2 73.7 -> 73.1-73.4 ms); the others
 // keep sqrt() and the division (config 3 90.0 -> 91.3 ms, config 4 139.1 -> 140.2 ms with them).
-// CRT_EXACT_SHORTCUTS = 0: off everywhere.
-#ifndef CRT_EXACT_SHORTCUTS
-#define CRT_EXACT_SHORTCUTS 1
-#endif
 template <bool FAST>
 __device__ __forceinline__ double sqrt_exact(double x) {
-    if (FAST && CRT_EXACT_SHORTCUTS) return sqrt_from_rsq(x, __builtin_amdgcn_rsq(x));
+    if (FAST) return sqrt_from_rsq(x, __builtin_amdgcn_rsq(x));
     return sqrt(x);
 }
 // 1 / s bit for bit: hipcc's gfx950 division 1 / s is div_scale, v_rcp_f64, two Newton steps
@@ -246,18 +235,14 @@ __device__ __forceinline__ double sqrt_exact(double x) {
 // scale and div_fixup returns its first operand (no NaN, inf, zero or denormal arises), so the
 // same operations without those three are that division's result; outside the range: 1 / s.
 __device__ __forceinline__ double recip_core(double s) {  // |s| in [2^-500, 2^500]
-#if CRT_EXACT_SHORTCUTS
     double y = __builtin_amdgcn_rcp(s);
     y = fma(y, fma(-s, y, 1.0), y);
     y = fma(y, fma(-s, y, 1.0), y);
     return fma(fma(-s, y, 1.0), y, y);
-#else
-    return 1 / s;
-#endif
 }
 template <bool FAST>
 __device__ __forceinline__ double recip_exact(double s) {
-    if (!FAST || !CRT_EXACT_SHORTCUTS) return 1 / s;
+    if (!FAST) return 1 / s;
     if (__builtin_expect(!(fabs(s) >= 0x1p-500 && fabs(s) <= 0x1p500), 0)) return 1 / s;
     return recip_core(s);
 }
@@ -993,7 +978,6 @@ __device__ __forceinline__ void walk(const SceneView& S, Stack<SE>& st, const do
         // values are monotone in the bounds (near(child) >= near(parent), far(child) <=
         // far(parent)), so the test fails for them at any t_max the culled one failed at.
         // Only node visits are added. The stack stays within depth + 1 levels: it is the same DFS.
-#if CRT_SPEC_MASKED
         // The loop is the wave's; parked lanes leave it through the exec mask (`run`). A lane
         // parks by popping like at any entered leaf and remembering the node (`pcur`); after the
         // loop its pop is undone. The recorded node is `pref` (~0u: none yet; the sentinel when
@@ -1048,58 +1032,6 @@ __device__ __forceinline__ void walk(const SceneView& S, Stack<SE>& st, const do
             cur = pcur;
             tp += stride;
         }
-#else
-        // The loop is the wave's (no per-lane exit): a parked lane runs the body again at the
-        // same node and stays parked (`run` is sticky), changing nothing but the dead level
-        // above its stack. The recorded node is `pref` (~0u: none yet; the sentinel when the
-        // lane entered it with no leaf recorded: traversal over), so the loop's exit test is one
-        // compare.
-        bool run = true;
-        uint32_t pref = ~0u;
-        do {
-            Uvec4 q0, q1;
-            fetch_nodef<TOP, LS>(S, cur, q0, q1);
-            w0 = q1.z;
-            w1 = q1.w;
-            const uint32_t top = *tp;  // speculative pop
-            if (COUNT && run) {
-                if (w1 != kSentinelW1) ctr.nodes++;
-                if (wave_leader()) ctr.it_walk++;
-            }
-            const float x0 = __builtin_fmaf(__uint_as_float(q0.x), R.inv32[0], -R.oinv32[0]);
-            const float x1 = __builtin_fmaf(__uint_as_float(q0.y), R.inv32[0], -R.oinv32[0]);
-            const float y0 = __builtin_fmaf(__uint_as_float(q0.z), R.inv32[1], -R.oinv32[1]);
-            const float y1 = __builtin_fmaf(__uint_as_float(q0.w), R.inv32[1], -R.oinv32[1]);
-            const float z0 = __builtin_fmaf(__uint_as_float(q1.x), R.inv32[2], -R.oinv32[2]);
-            const float z1 = __builtin_fmaf(__uint_as_float(q1.y), R.inv32[2], -R.oinv32[2]);
-            const float lo = vmax3(vmin(x0, x1), vmin(y0, y1), vmax_s(vmin(z0, z1), tmin32));
-            const float hi = vmin3(vmax(x0, x1), vmax(y0, y1), vmin(vmax(z0, z1), R.tmax32));
-            const float gap = hi - lo;
-            const float th = __builtin_fmaf(vmax_abs(lo, hi), 0x1p-19f, R.marg);
-            bool enter = gap > 0.f;
-            // parked lanes decide again too (the same decision; `run` keeps them parked anyway)
-            const bool unc = !(fabsf(gap) > th);
-            if (__builtin_expect(__ballot(unc) != 0, 0)) {
-                if (COUNT && wave_leader()) ctr.it_slow++;
-                if (unc) {
-                    if (COUNT && run) ctr.slow_nodes++;
-                    enter = slab64(node64(S, cur), o, d, tmin, R.tmax);
-                }
-            }
-            const bool inner = enter & (w1 < kLeafFlagF);
-            const uint32_t near = w1 | (__builtin_amdgcn_ubfe(R.neg, w0, 1) << kNodeFShift);
-            tp[stride] = static_cast<SE>(near ^ (1u << kNodeFShift));
-            const bool reached = enter & !inner;  // a leaf or the sentinel
-            const bool pend = pref != ~0u;
-            const bool rec = run & reached & !pend;  // the first leaf (or the sentinel)
-            const bool park = !run | (reached & (pend | (w1 == kSentinelW1)));
-            pref = rec ? cur : pref;
-            run = !park;
-            const uint32_t nxt = park ? cur : top;
-            cur = (inner & !park) ? near : nxt;
-            tp += (inner & !park) ? stride : (park ? 0 : -stride);
-        } while (__ballot(pref == ~0u) != 0);
-#endif
         // the recorded node's words (a leaf's primitive range, or the sentinel: traversal over)
         {
             Uvec4 q0, q1;
@@ -1168,12 +1100,8 @@ __device__ __forceinline__ void walk(const SceneView& S, Stack<SE>& st, const do
 // the entered leaf's primitives in order (bvh.h:635-652), then "return" to the DFS.
 // Sphere-only scenes store spheres in slot order, so the slot indexes them directly and the next
 // sphere is loaded while the current one is tested.
-// CMP (candidate compaction, CRT_COMPACT_CAND): the two-pass branches (sphere pairs, flat boxes)
-// stop after pass 1 and return the candidates (bit i = the leaf's primitive i; the lane stays in
-// kLeaf); compact_candidates() then tests every lane's candidates with the whole wave. Returns 0
-// when the leaf is done.
-template <typename SE, bool COUNT, bool TOP, bool LS, bool FAST = false, bool CMP = false>
-__device__ __forceinline__ uint32_t leaf_step(const SceneView& S, Stack<SE>& st, const double o[3],
+template <typename SE, bool COUNT, bool TOP, bool LS, bool FAST = false>
+__device__ __forceinline__ void leaf_step(const SceneView& S, Stack<SE>& st, const double o[3],
                                               const double d[3], double tmin, float tmin32, bool sphere_only, bool pairs,
                                               bool qfilter, bool qflat, Trav& R, LaneCounters& ctr) {
     const uint2 range = make_uint2(R.first, R.count);  // index, count
@@ -1204,10 +1132,6 @@ __device__ __forceinline__ uint32_t leaf_step(const SceneView& S, Stack<SE>& st,
             cand = sphere_pair_candidates(cand, rec, L);
         }
         cand &= ~(range.y & 1u);  // an odd count's last verdict is the slot after the leaf
-        if (CMP) {  // bit nbits - 1 - i -> bit i
-            cand = __builtin_bitreverse32(cand) >> (32 - nbits);
-            if (cand) return cand;
-        }
         while (cand) {
             if (COUNT) {
                 ctr.cand++;
@@ -1243,7 +1167,6 @@ __device__ __forceinline__ uint32_t leaf_step(const SceneView& S, Stack<SE>& st,
                                 __uint_as_float(q0.w), __uint_as_float(q1.x), __uint_as_float(q1.y)};
             cand |= static_cast<uint32_t>(flat_box_candidate<DevMinMax>(b, R.inv32, R.oinv32, tmin32, R.tmax32, R.marg)) << i;
         }
-        if (CMP && cand) return cand;
         while (cand) {
             if (COUNT) {
                 ctr.cand++;
@@ -1340,121 +1263,6 @@ __device__ __forceinline__ uint32_t leaf_step(const SceneView& S, Stack<SE>& st,
     }
     // the pop after the leaf was made by walk (R.cur is the next node, unless the stack was empty)
     R.state = R.sp < 0 ? kDone : kWalk;
-    return 0;
-}
-
-// Candidate compaction (the north star's ballot / prefix compaction, applied where the wave's
-// lanes are least used: pass 2 of the two-pass leaves, 25-33% lane utilization when each lane
-// tests its own 0-12 candidates). Every lane of the wave takes part: the deferred candidates of
-// all lanes (leaf_step<CMP>) become one dense list of (owner lane, primitive) items (bit-plane
-// ballots give each owner its exclusive prefix), the wave tests 64 items per iteration with the
-// owner's ray read across lanes (ds_bpermute), and each owner's closest hit is the minimum of
-// (t, primitive index) over its items (LDS atomics on t's bits, then on the index among the
-// items at that t). That equals the sequential loop: a candidate tested at the leaf-entry t_max
-// reports t iff the sequential loop's shrinking t_max would accept it at t (the sphere's first
-// root in (t_min, T) is the same for any T above it, and a parallelogram's t does not depend on
-// T), and the strict `t < t_max` update keeps the first of equal t in slot order.
-constexpr uint32_t kCmpCap = 128;  // items per wave and round (more: the per-lane loop)
-constexpr uint32_t kCmpWaveBytes = 64 * 8 + 64 * 4 + kCmpCap * 4;
-typedef __attribute__((address_space(3))) unsigned long long LdsU64;
-typedef __attribute__((address_space(3))) uint32_t LdsU32;
-
-template <bool LS, bool QUAD, bool COUNT, bool FAST>
-__device__ __forceinline__ void compact_candidates(const SceneView& S, uint32_t lds_cmp, const double o[3],
-                                                   const double d[3], double tmin, uint32_t defer, Trav& R,
-                                                   LaneCounters& ctr) {
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t base = lds_cmp + (threadIdx.x >> 6) * kCmpWaveBytes;
-    LdsU64* const tkey = (LdsU64*)static_cast<uintptr_t>(base);
-    LdsU32* const best = (LdsU32*)static_cast<uintptr_t>(base + 64 * 8);
-    LdsU32* const list = (LdsU32*)static_cast<uintptr_t>(base + 64 * 12);
-    // exclusive prefix of the candidate counts over the lanes (counts <= 32: six bit planes)
-    const uint32_t n = static_cast<uint32_t>(__builtin_popcount(defer));
-    uint32_t pre = 0, total = 0;
-#pragma unroll
-    for (uint32_t b = 0; b < 6; ++b) {
-        const uint64_t m = __ballot((n >> b) & 1u);
-        pre += __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32), __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0u)) << b;
-        total += static_cast<uint32_t>(__popcll(m)) << b;
-    }
-    if (COUNT) ctr.cand += n;
-    const double ia = QUAD ? 0.0 : recip_a<FAST>(R.a);
-    if (total > kCmpCap) {  // the per-lane loop of leaf_step
-        uint32_t m = defer;
-        while (m) {
-            if (COUNT && wave_leader()) ctr.it_cand++;
-            const uint32_t i = R.first + static_cast<uint32_t>(__builtin_ctz(m));
-            m &= m - 1;
-            double t;
-            bool h;
-            if constexpr (QUAD) h = hit_quad(lds_rec<DevQuad>(S.quads_lds + (i << 7)), o, d, tmin, R.tmax, t);
-            else h = hit_sphere<false>(sphere_at<LS>(S, i), o, d, R.a, ia, tmin, R.tmax, 0.0, 0.0, t);
-            if (h) {
-                R.tmax = t;
-                R.tmax32 = tmax_f32(t);
-                R.ref = (QUAD ? kRefQuad : 0u) | i;
-                R.found = true;
-            }
-        }
-        if (defer) R.state = R.sp < 0 ? kDone : kWalk;
-        return;
-    }
-    tkey[lane] = ~0ull;
-    best[lane] = ~0u;
-    for (uint32_t m = defer, k = pre; m; m &= m - 1, ++k) list[k] = lane | (static_cast<uint32_t>(__builtin_ctz(m)) << 6);
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    unsigned long long key[kCmpCap / 64];
-    uint32_t own[kCmpCap / 64], idx[kCmpCap / 64];
-#pragma unroll
-    for (uint32_t it = 0; it < kCmpCap / 64; ++it) {
-        key[it] = ~0ull;
-        own[it] = 0;
-        idx[it] = 0;
-        if (it * 64 >= total) continue;  // wave-uniform
-        if (COUNT && wave_leader()) ctr.it_cand++;
-        const uint32_t j = it * 64 + lane;
-        const bool live = j < total;
-        const uint32_t item = list[live ? j : 0];
-        own[it] = item & 63;
-        idx[it] = item >> 6;
-        const int src = static_cast<int>(own[it]);
-        const double oo[3] = {__shfl(o[0], src), __shfl(o[1], src), __shfl(o[2], src)};
-        const double dd[3] = {__shfl(d[0], src), __shfl(d[1], src), __shfl(d[2], src)};
-        const double tmax = __shfl(R.tmax, src);
-        const uint32_t i = __shfl(R.first, src) + idx[it];
-        double t = 0;
-        bool h;
-        if constexpr (QUAD) {
-            h = hit_quad(lds_rec<DevQuad>(S.quads_lds + (i << 7)), oo, dd, tmin, tmax, t);
-        } else {
-            const double a = __shfl(R.a, src), iao = __shfl(ia, src);
-            h = hit_sphere<false>(sphere_at<LS>(S, i), oo, dd, a, iao, tmin, tmax, 0.0, 0.0, t);
-        }
-        if (live && h) {
-            key[it] = static_cast<unsigned long long>(__double_as_longlong(t));  // t > t_min > 0
-            __hip_atomic_fetch_min(tkey + own[it], key[it], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-        }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-#pragma unroll
-    for (uint32_t it = 0; it < kCmpCap / 64; ++it)
-        if (key[it] != ~0ull && key[it] == tkey[own[it]])
-            __hip_atomic_fetch_min(best + own[it], idx[it], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    if (defer) {
-        const unsigned long long k = tkey[lane];
-        if (k != ~0ull) {
-            const double t = __longlong_as_double(static_cast<long long>(k));
-            R.tmax = t;
-            R.tmax32 = tmax_f32(t);
-            R.ref = (QUAD ? kRefQuad : 0u) | (R.first + best[lane]);
-            R.found = true;
-        }
-        R.state = R.sp < 0 ? kDone : kWalk;
-    }
 }
 
 __device__ __forceinline__ uint32_t owned_row(const Work& w, uint32_t k) {
@@ -1639,67 +1447,26 @@ __device__ __forceinline__ void stage_lds(unsigned char* dst, const void* src, u
 #ifndef CRT_SHADE_BATCH
 #define CRT_SHADE_BATCH 48
 #endif
-// pass 2 of the two-pass leaves by the whole wave over a compacted candidate list
-// (compact_candidates); 0: each lane tests its own candidates
-#ifndef CRT_COMPACT_CAND
-#define CRT_COMPACT_CAND 0
-#endif
 constexpr int kShadeBatch = CRT_SHADE_BATCH;
-// ...or once at least kShadeMin are and no more than kPendingMax lanes still traverse (off by
-// default: 56/32/8, 64/40/8 and 56/24/4 all measured slower than 48 alone)
-#ifndef CRT_SHADE_MIN
-#define CRT_SHADE_MIN 64
-#endif
-#ifndef CRT_PENDING_MAX
-#define CRT_PENDING_MAX 0
-#endif
-constexpr int kShadeMin = CRT_SHADE_MIN, kPendingMax = CRT_PENDING_MAX;
 
-#ifndef CRT_TOP_TREELET
-#define CRT_TOP_TREELET 1
-#endif
-constexpr bool kTopTreelet = CRT_TOP_TREELET != 0;
-// speculative walk (walk(): lanes that found their first leaf walk on to the next one); the
-// instrumented pass (COUNT) keeps the plain walk, so its node counts are the reference's
-// (CRT_COUNT_SPEC=1: the instrumented pass walks speculatively too, for phase timings; its node
-// counts then include the speculative visits)
-#ifndef CRT_SPEC_WALK
-#define CRT_SPEC_WALK 1
-#endif
-#ifndef CRT_COUNT_SPEC
-#define CRT_COUNT_SPEC 0
-#endif
-constexpr bool kSpecWalk = CRT_SPEC_WALK != 0, kCountSpec = CRT_COUNT_SPEC != 0;
+// HBM-scene kernels keep the top of the node array in LDS (CRT_NO_LDS_TOP=1 at run time: none)
+constexpr bool kTopTreelet = true;
+// The timed kernels walk speculatively (walk(): lanes that found their first leaf walk on to the
+// next one). The instrumented pass (COUNT) walks like the reference by default, so its node counts
+// are the reference's (the algorithmic-byte basis); with Work::count_spec (CRT_COUNT_SPEC=1 at run
+// time) it walks speculatively too, for the timed kernel's phase timings and lane utilization (its
+// node counts then include the speculative visits).
 // Static wave priority per phase (s_setprio 0-3; the SQ issues a ready instruction of the highest
 // priority wave first, then the oldest): the traversal phases are dependency chains (LDS read ->
 // test -> next address), the shade and path-start phases have more independent work to fill in.
 // Config 2 (ms/frame, one box): none 87.9; walk 1 86.6; walk+leaf 1 85.6; walk 2 / leaf 1 85.6;
 // walk 1 / leaf 2 85.6; walk 2 / leaf 2 / start 1 85.4; walk 3 / leaf 2 / start 1 (kept) 85.3;
 // walk 1 / leaf 1 / start 1 86.0.
-#ifndef CRT_PRIO_WALK
-#define CRT_PRIO_WALK 3
-#endif
-#ifndef CRT_PRIO_LEAF
-#define CRT_PRIO_LEAF 2
-#endif
-#ifndef CRT_PRIO_SHADE
-#define CRT_PRIO_SHADE 0
-#endif
-#ifndef CRT_PRIO_INIT
-#define CRT_PRIO_INIT 1
-#endif
-constexpr int kPrioWalk = CRT_PRIO_WALK, kPrioLeaf = CRT_PRIO_LEAF, kPrioShade = CRT_PRIO_SHADE,
-              kPrioInit = CRT_PRIO_INIT;
+constexpr int kPrioWalk = 3, kPrioLeaf = 2, kPrioShade = 0, kPrioInit = 1;
 template <int P>
 __device__ __forceinline__ void set_prio() {
     if constexpr ((kPrioWalk | kPrioLeaf | kPrioShade | kPrioInit) != 0) __builtin_amdgcn_s_setprio(P);
 }
-// per-round lane counts in the instrumented pass (printed under CRT_DEBUG_COUNTERS); off by default:
-// their atomics shift the instrumented pass's phase timings
-#ifndef CRT_ROUND_COUNTERS
-#define CRT_ROUND_COUNTERS 0
-#endif
-constexpr bool kRoundCounters = CRT_ROUND_COUNTERS != 0;
 
 // PM (primitive mix): 0 sphere-only scenes (every parallelogram path compiled out), 1 any scene,
 // 2 parallelogram-only scenes of axis-aligned parallelograms (LDS scenes: the flat-box filter
@@ -1707,7 +1474,7 @@ constexpr bool kRoundCounters = CRT_ROUND_COUNTERS != 0;
 // W5: 5 waves per SIMD (96 VGPRs, ~40-48 of them spilled), launched for sphere-only and
 // flat-parallelogram LDS scenes whose LDS copy leaves room for five blocks per CU (dispatch_render)
 template <typename SE, bool GSTACK, bool LSCENE, bool COUNT, int PM, bool W5>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W5 ? CRT_MANY_WAVES : LSCENE ? CRT_WAVES_PER_EU_LDS : CRT_WAVES_PER_EU, 8))) void render_kernel(
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W5 ? kManyWaves : LSCENE ? CRT_WAVES_PER_EU_LDS : CRT_WAVES_PER_EU, 8))) void render_kernel(
     SceneView Sg, CamView C, Work W, double* __restrict__ partial, SE* __restrict__ gstack,
     Counters* __restrict__ counters) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1717,9 +1484,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W5 ? CRT
     // sqrt / reciprocal expansions without range fix-ups (sqrt_exact, recip_exact): measured
     // faster only in the five-wave sphere-only instance
     constexpr bool kFast = kSphOnly && W5;
-    // candidate compaction: the sphere-only and flat-parallelogram instances (their two-pass
-    // leaves); flat boxes are LDS-scene only
-    constexpr bool kCompact = CRT_COMPACT_CAND != 0 && (kSphOnly || (kFlatOnly && LSCENE));
     SceneView S = Sg;
     if (LSCENE) {  // f32 nodes at LDS offset 0 (fetch_nodef: a node's LDS address is its ref)
         if (static_cast<uint32_t>(reinterpret_cast<uintptr_t>((LdsByte*)smem)) != 0) __builtin_trap();
@@ -1787,7 +1551,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W5 ? CRT
     // -> 72.6 ms, config 3 0.4% slower with it in the flat instance); shade adds a path's
     // contribution to a zeroed local (0 + x = x) that then goes into the LDS sum: the same
     // additions as acc + x
-    constexpr bool kAccLds = kFast && CRT_ACC_LDS;
+    constexpr bool kAccLds = kFast;
     typedef __attribute__((address_space(3))) double LdsDouble;
     LdsDouble* const acc_l = (LdsDouble*)static_cast<uintptr_t>(W.lds_acc + threadIdx.x * 8);
     if (kAccLds) {
@@ -1897,7 +1661,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W5 ? CRT
         // traversal rounds (walk to the next entered leaf, test it) until enough lanes hold a
         // finished ray, or none is traversing
         while (true) {
-            if (COUNT && kRoundCounters) {
+            if (COUNT && W.round_counters) {
                 const unsigned long long nw = __popcll(__ballot(R.state == kWalk));
                 if (wave_leader()) {
                     atomicAdd(&counters->rounds, 1ull);
@@ -1907,34 +1671,36 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W5 ? CRT
             if (COUNT) cw -= static_cast<uint32_t>(wall_clock64());
             set_prio<kPrioWalk>();
             if (!W.exact_slab && __ballot(R.state == kWalk && (R.neg & kZeroDir)) == 0) {
-                if (R.state == kWalk) walk<SE, COUNT, false, kTopTreelet && !LSCENE, LSCENE, GSTACK, kSpecWalk && (!COUNT || kCountSpec)>(S, st, P.o, P.d, C.t_min, tmin32, R, ctr);
+                if (R.state == kWalk) {
+                    if (!COUNT || W.count_spec)
+                        walk<SE, COUNT, false, kTopTreelet && !LSCENE, LSCENE, GSTACK, true>(S, st, P.o, P.d, C.t_min, tmin32, R, ctr);
+                    else
+                        walk<SE, COUNT, false, kTopTreelet && !LSCENE, LSCENE, GSTACK, false>(S, st, P.o, P.d, C.t_min, tmin32, R, ctr);
+                }
             } else {
-                if (R.state == kWalk) walk<SE, COUNT, true, kTopTreelet && !LSCENE, LSCENE, GSTACK, kSpecWalk && (!COUNT || kCountSpec)>(S, st, P.o, P.d, C.t_min, tmin32, R, ctr);
+                if (R.state == kWalk) walk<SE, COUNT, true, kTopTreelet && !LSCENE, LSCENE, GSTACK, false>(S, st, P.o, P.d, C.t_min, tmin32, R, ctr);
             }
             if (COUNT) cw += static_cast<uint32_t>(wall_clock64());
             set_prio<kPrioLeaf>();
-            if (COUNT && kRoundCounters) {
+            if (COUNT && W.round_counters) {
                 const unsigned long long nl = __popcll(__ballot(R.state == kLeaf));
                 if (wave_leader()) atomicAdd(&counters->round_leaves, nl);
             }
             if (COUNT) cl -= static_cast<uint32_t>(wall_clock64());
-            uint32_t defer = 0;
-            if (R.state == kLeaf) defer = leaf_step<SE, COUNT, kTopTreelet && !LSCENE, LSCENE, kFast, kCompact>(S, st, P.o, P.d, C.t_min, tmin32, kSphOnly || (!kFlatOnly && W.sphere_only != 0), !kFlatOnly && W.spheres_f32 != 0, kFlatOnly || (!kSphOnly && W.quads_f32 != 0), kFlatOnly || (!kSphOnly && W.quads_flat != 0), R, ctr);
-            if (kCompact && __ballot(defer != 0) != 0)
-                compact_candidates<LSCENE, kFlatOnly, COUNT, kFast>(S, W.lds_cmp, P.o, P.d, C.t_min, defer, R, ctr);
+            if (R.state == kLeaf) leaf_step<SE, COUNT, kTopTreelet && !LSCENE, LSCENE, kFast>(S, st, P.o, P.d, C.t_min, tmin32, kSphOnly || (!kFlatOnly && W.sphere_only != 0), !kFlatOnly && W.spheres_f32 != 0, kFlatOnly || (!kSphOnly && W.quads_f32 != 0), kFlatOnly || (!kSphOnly && W.quads_flat != 0), R, ctr);
             if (COUNT) cl += static_cast<uint32_t>(wall_clock64());
             const uint64_t pending = __ballot(R.state == kWalk);
             const uint64_t finished = __ballot(R.state == kDone);
             const int nfin = __popcll(finished);
-            if (COUNT && kRoundCounters && wave_leader()) atomicAdd(&counters->round_done, static_cast<unsigned long long>(nfin));
-            if (pending == 0 || nfin >= kShadeBatch || (__popcll(pending) <= kPendingMax && nfin >= kShadeMin)) break;
+            if (COUNT && W.round_counters && wave_leader()) atomicAdd(&counters->round_done, static_cast<unsigned long long>(nfin));
+            if (pending == 0 || nfin >= kShadeBatch) break;
         }
         const uint64_t m_done = __ballot(R.state == kDone);
         if (COUNT && t_first_idle == 0 && __ballot(R.state == kIdle) != 0) t_first_idle = wall_clock64();
         if (m_done == 0) break;  // every lane idle: the queue is dry
         if (COUNT) cs -= static_cast<uint32_t>(wall_clock64());
         set_prio<kPrioShade>();
-        if (COUNT && kRoundCounters && wave_leader()) atomicAdd(&counters->shade_rounds, 1ull);
+        if (COUNT && W.round_counters && wave_leader()) atomicAdd(&counters->shade_rounds, 1ull);
         if (COUNT && ((ctr.rays | ctr.nodes | ctr.sphere_tests | ctr.quad_tests | ctr.it_walk | ctr.it_leaf |
                        ctr.it_shade | ctr.slow_nodes | ctr.it_slow | ctr.cand | ctr.it_cand) & 0x80000000u))
             flush_counts(ctr, counters);
@@ -2005,8 +1771,7 @@ __global__ __launch_bounds__(256) void resolve_kernel(const double* __restrict__
     const uint64_t band = static_cast<uint64_t>(W.bh) * W.bw;
     if (i >= band) return;
     const uint32_t k = W.k0 + static_cast<uint32_t>(i / W.bw), col = W.col0 + static_cast<uint32_t>(i % W.bw);
-    const uint32_t row = owned_row(W, k);
-    const size_t pix = static_cast<size_t>(row) * w + col;
+    const size_t pix = static_cast<size_t>(W.packed ? k : owned_row(W, k)) * w + col;
     const size_t plane = band * 3;
     double r = partial[i * 3 + 0], g = partial[i * 3 + 1], b = partial[i * 3 + 2];
     for (uint32_t c = 1; c < W.chunks; ++c) {
@@ -2028,6 +1793,19 @@ __global__ __launch_bounds__(256) void resolve_kernel(const double* __restrict__
 constexpr double kPpmScale = 255 + 0.999999;
 constexpr int32_t kPpmRedo = INT32_MIN + 1;
 
+__device__ __forceinline__ int32_t ppm_channel(double c, double L) {
+    const double x = c / (1 + L);
+    const double s = sqrt(x);
+    const double v = kPpmScale * s;
+    if (!(v >= 0 && v < 2147483648.0)) return kPpmRedo;
+    if (s < 0x1p-1000) return 0;  // pow(x, 0.5) is below 2^-999 too
+    const uint64_t bits = static_cast<uint64_t>(__double_as_longlong(s));
+    const double lo = __longlong_as_double(static_cast<long long>(bits - 2));
+    const double hi = __longlong_as_double(static_cast<long long>(bits + 2));
+    return static_cast<int32_t>(kPpmScale * lo) == static_cast<int32_t>(kPpmScale * hi) ? static_cast<int32_t>(v)
+                                                                                          : kPpmRedo;
+}
+
 __global__ __launch_bounds__(256) void ppm_kernel(const double* __restrict__ rgb, uint64_t n,
                                                   int32_t* __restrict__ out) {
     const uint64_t i = static_cast<uint64_t>(blockIdx.x) * 256 + threadIdx.x;
@@ -2035,24 +1813,32 @@ __global__ __launch_bounds__(256) void ppm_kernel(const double* __restrict__ rgb
     const double c[3] = {rgb[3 * i], rgb[3 * i + 1], rgb[3 * i + 2]};
     const double L = 0.2126 * c[0] + 0.7152 * c[1] + 0.0722 * c[2];
 #pragma unroll
+    for (int k = 0; k < 3; ++k) out[3 * i + k] = ppm_channel(c[k], L);
+}
+
+// The same values as 8-bit bytes (the fused output of crt_render_ppm: 3 B a pixel cross xGMI and
+// PCIe instead of 24). A pixel with a value the kernel cannot settle, or outside [0, 255] (a NaN
+// pixel prints INT_MIN), is listed in redo = [count, pixel...] (at most cap) for the host.
+__global__ __launch_bounds__(256) void ppm8_kernel(const double* __restrict__ rgb, uint64_t n,
+                                                   uint8_t* __restrict__ out, uint32_t* __restrict__ redo,
+                                                   uint32_t cap) {
+    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * 256 + threadIdx.x;
+    if (i >= n) return;
+    const double c[3] = {rgb[3 * i], rgb[3 * i + 1], rgb[3 * i + 2]};
+    const double L = 0.2126 * c[0] + 0.7152 * c[1] + 0.0722 * c[2];
+    int32_t q[3];
+    bool ok = true;
+#pragma unroll
     for (int k = 0; k < 3; ++k) {
-        const double x = c[k] / (1 + L);
-        const double s = sqrt(x);
-        const double v = kPpmScale * s;
-        int32_t q;
-        if (!(v >= 0 && v < 2147483648.0)) {
-            q = kPpmRedo;
-        } else if (s < 0x1p-1000) {
-            q = 0;  // pow(x, 0.5) is below 2^-999 too
-        } else {
-            const uint64_t bits = static_cast<uint64_t>(__double_as_longlong(s));
-            const double lo = __longlong_as_double(static_cast<long long>(bits - 2));
-            const double hi = __longlong_as_double(static_cast<long long>(bits + 2));
-            q = static_cast<int32_t>(kPpmScale * lo) == static_cast<int32_t>(kPpmScale * hi)
-                    ? static_cast<int32_t>(v) : kPpmRedo;
-        }
-        out[3 * i + k] = q;
+        q[k] = ppm_channel(c[k], L);
+        ok = ok && q[k] >= 0 && q[k] <= 255;
     }
+    if (!ok) {
+        const uint32_t j = atomicAdd(redo, 1u);
+        if (j < cap) redo[1 + j] = static_cast<uint32_t>(i);
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) out[3 * i + k] = ok ? static_cast<uint8_t>(q[k]) : 0;
 }
 
 // Closest-hit queries (BVH::hit_by for an arbitrary ray batch).
@@ -2361,23 +2147,11 @@ static uint32_t count_owned(uint32_t h, uint32_t rb, uint32_t tc, uint32_t ti) {
 
 static size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
 
-constexpr size_t kAccBytes = CRT_ACC_LDS ? 3 * dev::kBlock * sizeof(double) : 0;  // five-wave sphere-only pixel sums
-constexpr size_t kCmpBytes = CRT_COMPACT_CAND ? (dev::kBlock / 64) * dev::kCmpWaveBytes : 0;  // compaction lists
-#ifndef CRT_FIVE_WAVES
-#define CRT_FIVE_WAVES 1
-#endif
-constexpr bool kFiveWaves = CRT_FIVE_WAVES != 0;  // the 5-wave instance for small sphere-only LDS scenes
-#ifndef CRT_LDS_BUDGET_KB
-#define CRT_LDS_BUDGET_KB 40
-#endif
-constexpr size_t kLdsSceneBudget = CRT_LDS_BUDGET_KB * 1024;  // scene + stack per block
+constexpr size_t kAccBytes = 3 * dev::kBlock * sizeof(double);  // five-wave sphere-only pixel sums
+constexpr size_t kLdsSceneBudget = 40 * 1024;  // scene + stack per block
 // sphere-only LDS scenes also stage the f64 spheres (pass 2's exact tests, shading) when the block
 // still fits 40 KB: rtow 40.6 KB, 84.7 vs 85.4 ms with them in HBM / L1 (v12; round 1's layout,
 // with even-aligned filter records to make room, had measured the opposite)
-#ifndef CRT_SPH64_LDS
-#define CRT_SPH64_LDS 1
-#endif
-constexpr bool kSph64Lds = CRT_SPH64_LDS != 0;
 constexpr size_t kLdsStackBudget = 32 * 1024 * dev::kBlock / 256;
 
 // Partial-sum budget per launch (bytes): the owned frame is rendered in bands whose partial sums
@@ -2396,13 +2170,9 @@ static int launch_render(const crt_scene* s, int device, const crt_camera* cam, 
     dev::Work W = w0;
     W.lds_cam = static_cast<uint32_t>(align16(lds));  // the camera copy after the rest
     lds = W.lds_cam + align16(sizeof(dev::CamView));
-    if (W5 && PM == 0 && CRT_ACC_LDS) {  // then the pixel sums (render_kernel: kAccLds)
+    if (W5 && PM == 0) {  // then the pixel sums (render_kernel: kAccLds)
         W.lds_acc = static_cast<uint32_t>(align16(lds));
         lds = W.lds_acc + kAccBytes;
-    }
-    if (CRT_COMPACT_CAND && (PM == 0 || (PM == 2 && LSCENE))) {  // then the compaction lists
-        W.lds_cmp = static_cast<uint32_t>(align16(lds));
-        lds = W.lds_cmp + kCmpBytes;
     }
     const uint64_t pixels = static_cast<uint64_t>(W.owned_rows) * cam->image_w;
     // Sample chunks: a function of spp ONLY, so every pixel's sum is grouped identically whatever
@@ -2614,12 +2384,12 @@ static int dispatch_render(const crt_scene* s, int device, const crt_camera* cam
         // too (config 2: 73.7 ms at five waves without them vs 75.8 at four with them; config 3:
         // 89.8 vs 92.6); the others four, with up to 40 KB (the general instance at five: config
         // 3 116.5 vs 100.6 ms).
-        const size_t budget5 = 160 * 1024 / CRT_MANY_WAVES;  // blocks of four waves a CU
-        const bool w5 = (W.sphere_only || W.quads_flat) && kFiveWaves && std::getenv("CRT_FOUR_WAVES") == nullptr &&
-                        stack_at(scene_bytes) + stack_bytes + cam_bytes + (W.sphere_only ? kAccBytes : 0) + kCmpBytes <= budget5;
+        const size_t budget5 = 160 * 1024 / dev::kManyWaves;  // blocks of four waves a CU
+        const bool w5 = (W.sphere_only || W.quads_flat) && std::getenv("CRT_FOUR_WAVES") == nullptr &&
+                        stack_at(scene_bytes) + stack_bytes + cam_bytes + (W.sphere_only ? kAccBytes : 0) <= budget5;
         const size_t budget = w5 ? budget5 : kLdsSceneBudget;
         const uint32_t sph64 = static_cast<uint32_t>(s->spheres.size() * sizeof(DevSphere));
-        if (W.spheres_f32 && kSph64Lds && stack_at(scene_bytes + sph64) + stack_bytes + cam_bytes + (w5 ? kAccBytes : 0) + kCmpBytes <= budget)
+        if (W.spheres_f32 && stack_at(scene_bytes + sph64) + stack_bytes + cam_bytes + (w5 ? kAccBytes : 0) <= budget)
             W.bytes_sph64 = sph64;
         W.lds_stack = stack_at(scene_bytes + W.bytes_sph64);
         const size_t lds = W.lds_stack + stack_bytes;
@@ -2641,7 +2411,7 @@ static int dispatch_render(const crt_scene* s, int device, const crt_camera* cam
         return no_top ? 0u : static_cast<uint32_t>(std::min(all_nodes, room / sizeof(DevNodeF) * sizeof(DevNodeF)));
     };
     if (stack_bytes <= kLdsStackBudget && std::getenv("CRT_FORCE_GSTACK") == nullptr) {
-        const size_t taken = stack_bytes + 2 * level + (W.sphere_only ? kCmpBytes : 0);
+        const size_t taken = stack_bytes + 2 * level;
         const size_t room = per_block > taken ? per_block - taken : 0;
         W.ntop = top_bytes(room);
         W.lds_nodes = 0;
@@ -2667,6 +2437,7 @@ int device_render(const crt_scene* s, int device, const crt_camera* cam, const c
         return fail(CRT_E_INVALID, "image has more than 2^32-1 pixels");
     crt_tiling tl{1, 1, 0, 0};
     if (t) tl = *t;
+    if (tl.flags & ~CRT_TILING_PACKED) return fail(CRT_E_INVALID, "unknown tiling flags");
     if (tl.row_block == 0 || tl.tile_count == 0 || tl.tile_index >= tl.tile_count)
         return fail(CRT_E_INVALID, "bad tiling");
     DeviceGuard g(device);
@@ -2675,6 +2446,7 @@ int device_render(const crt_scene* s, int device, const crt_camera* cam, const c
     W.tile_count = tl.tile_count;
     W.tile_index = tl.tile_index;
     W.owned_rows = count_owned(cam->image_h, tl.row_block, tl.tile_count, tl.tile_index);
+    W.packed = (tl.flags & CRT_TILING_PACKED) ? 1u : 0u;
     if (W.owned_rows == 0 || cam->samples_per_pixel == 0) {
         if (count_stats) *count_stats = crt_render_stats{};
         if (cam->samples_per_pixel == 0 && d_rgb && W.owned_rows) {
@@ -2683,7 +2455,7 @@ int device_render(const crt_scene* s, int device, const crt_camera* cam, const c
                                        std::numeric_limits<double>::quiet_NaN());
             for (uint32_t k = 0; k < W.owned_rows; ++k) {
                 uint32_t blk = k / W.row_block, in = k % W.row_block;
-                uint32_t row = (blk * W.tile_count + W.tile_index) * W.row_block + in;
+                uint32_t row = (tl.flags & CRT_TILING_PACKED) ? k : (blk * W.tile_count + W.tile_index) * W.row_block + in;
                 HIP_TRY(hipMemcpyAsync(d_rgb + static_cast<size_t>(row) * cam->image_w * 3, nanrow.data(),
                                        nanrow.size() * 8, hipMemcpyHostToDevice,
                                        static_cast<hipStream_t>(stream)));
@@ -2698,6 +2470,8 @@ int device_render(const crt_scene* s, int device, const crt_camera* cam, const c
     // the flat-box filter is the walk's f32 node test: it needs the walk's f32 range (f32_ok)
     W.quads_flat = (W.quads_f32 && s->dev[device].quads_flat_ok && s->dev[device].f32_ok) ? 1u : 0u;
     W.exact_slab = (s->exact_slab || std::getenv("CRT_EXACT_SLAB") != nullptr) ? 1u : 0u;
+    W.count_spec = std::getenv("CRT_COUNT_SPEC") != nullptr ? 1u : 0u;
+    W.round_counters = std::getenv("CRT_ROUND_COUNTERS") != nullptr ? 1u : 0u;
     hipStream_t st = static_cast<hipStream_t>(stream);
     if (count_stats) HIP_TRY(hipStreamCreate(&st));
     int r;
@@ -2783,17 +2557,62 @@ int device_ppm_values(int device, const double* d_rgb, size_t n, int32_t* h_valu
     return CRT_OK;
 }
 
-// crt_render: the whole frame over devices [0, n). Rows are dealt in 4-row blocks (row r on device
-// (r / 4) % n, crt_tiling{4, n, d}); the scene is uploaded to every device concurrently (one host
-// thread per device, one copy of the staged image each); each device renders its rows into its
-// own frame buffer on its own stream; device 0's stream then waits for each device and pulls that
-// device's row blocks into its frame with ONE strided peer copy (hipMemcpy2DAsync over xGMI: the
-// blocks are 4 rows apart by n x 4 rows), and the assembled frame crosses PCIe once. Frames are
-// bit-identical for any n (per-sample RNG, spp-only sample chunks).
+// Peer access from device `to` to device `from`'s memory, enabled once per pair per process
+// (hipDeviceEnablePeerAccess fails with AlreadyEnabled on a repeat call; HIP keeps such an error as
+// the thread's last error, so it is read off here, not left for a later hipGetLastError).
+static void enable_peer_once(int to, int from) {
+    static std::mutex mu;
+    static bool done[kMaxDevices][kMaxDevices] = {};
+    std::lock_guard<std::mutex> lk(mu);
+    if (done[to][from]) return;
+    done[to][from] = true;
+    int can = 0;
+    if (hipDeviceCanAccessPeer(&can, to, from) != hipSuccess || !can) {
+        (void)hipGetLastError();
+        return;  // the copies still work, staged by the runtime
+    }
+    DeviceGuard g(to);
+    if (hipDeviceEnablePeerAccess(from, 0) != hipSuccess) (void)hipGetLastError();
+}
+
+// Device d's owned rows (crt_tiling{rb, n, d}) are packed in its buffer; copy them to their frame
+// rows in `dst` (on device 0): full rb-row blocks with one strided copy (rb rows apart in the
+// source, n x rb rows apart in the frame), a short last block on its own. bytes_per_row: one row.
+static hipError_t gather_packed(char* dst, const char* src, size_t H, size_t rb, int n, int d,
+                                size_t bytes_per_row, hipStream_t st) {
+    const size_t first = static_cast<size_t>(d) * rb, step = static_cast<size_t>(n) * rb;
+    if (first >= H) return hipSuccess;
+    const size_t blocks = (H - first + step - 1) / step;     // blocks of device d
+    const size_t last = first + (blocks - 1) * step;         // frame row of its last block
+    const size_t full = last + rb <= H ? blocks : blocks - 1; // blocks with all rb rows
+    hipError_t e = hipSuccess;
+    if (full)
+        e = hipMemcpy2DAsync(dst + first * bytes_per_row, step * bytes_per_row, src, rb * bytes_per_row,
+                             rb * bytes_per_row, full, hipMemcpyDeviceToDevice, st);
+    if (e == hipSuccess && full < blocks)
+        e = hipMemcpyAsync(dst + last * bytes_per_row, src + full * rb * bytes_per_row, (H - last) * bytes_per_row,
+                           hipMemcpyDeviceToDevice, st);
+    return e;
+}
+
+// crt_render / crt_render_ppm: the whole frame over devices [0, n). Rows are dealt in 4-row
+// blocks (row r on device (r / 4) % n, crt_tiling{4, n, d}); the scene is uploaded to every device
+// concurrently (one host thread per device, one copy of the staged image each); each device renders
+// its own rows only, packed (CRT_TILING_PACKED: a device holds its share of the frame, 1/n of it)
+// on its own stream; device 0's stream then waits for each device and pulls that device's row
+// blocks into the frame with ONE strided peer copy (hipMemcpy2DAsync over xGMI), and the assembled
+// frame crosses PCIe once. Frames are bit-identical for any n (per-sample RNG, spp-only sample
+// chunks).
+//   h_rgb (f64 frame, crt_render): 24 B a pixel cross xGMI and PCIe; device 0 renders straight
+//     into the frame.
+//   h_ppm (int32 PPM values, crt_render_ppm; image.h:38-56, rgb.h:90-115): every device converts
+//     its rows to 8-bit PPM values before the gather (ppm8_kernel), so 3 B a pixel cross xGMI and
+//     PCIe; the few pixels the kernel leaves to the host (NaN, out of range, or within 2 ulps of
+//     an integer step) are recomputed from their f64 values with std::pow (ppm_pixel_host).
 // CRT_EMULATE_DEVICES=k (tests): k logical devices all on device 0, through the same tiling and
 // gather code.
-int render_multi(crt_scene* s, const crt_camera* cam, int num_devices, double* h_rgb,
-                 crt_render_stats* stats) {
+static int render_multi_impl(crt_scene* s, const crt_camera* cam, int num_devices, double* h_rgb,
+                             int32_t* h_ppm, crt_render_stats* stats) {
     int avail = 0;
     if (hipGetDeviceCount(&avail) != hipSuccess || avail == 0)
         return fail(CRT_E_NODEVICE, "no HIP device visible (the render path has no CPU fallback)");
@@ -2805,69 +2624,95 @@ int render_multi(crt_scene* s, const crt_camera* cam, int num_devices, double* h
         emulate = true;
     }
     const int n = num_devices;
+    const bool ppm = h_ppm != nullptr;
     auto phys = [&](int d) { return emulate ? 0 : d; };
     const size_t W = cam->image_w, H = cam->image_h;
-    const size_t frame = H * W * 3;
     const uint32_t rb = 4;  // 4-row blocks: 800 rows split exactly over 1, 2, 4, 8 devices
-    // 1. concurrent uploads, one thread per physical device
+    // 1. concurrent uploads, one thread per physical device; a worker's error message is taken
+    // from its own thread (crt_last_error is per thread) and raised again on this one
     const int n_phys = emulate ? 1 : n;
     std::vector<int> urc(n_phys, CRT_OK);
+    std::vector<std::string> umsg(n_phys);
     {
         std::vector<std::thread> th;
-        for (int d = 0; d < n_phys; ++d) th.emplace_back([&, d] { urc[d] = device_upload(s, d); });
+        for (int d = 0; d < n_phys; ++d)
+            th.emplace_back([&, d] {
+                urc[d] = device_upload(s, d);
+                if (urc[d]) umsg[d] = crt_last_error();
+            });
         for (auto& t : th) t.join();
     }
     for (int d = 0; d < n_phys; ++d)
-        if (urc[d]) return urc[d];
-    // 2. render: each logical device into its own frame buffer on its own stream
+        if (urc[d]) return fail(urc[d], "device " + std::to_string(d) + ": " + umsg[d]);
+    // 2. render: each logical device its own rows on its own stream (f64 mode: device 0 into the
+    // whole frame, the others packed; ppm mode: every device packed, then to 8-bit values)
     std::vector<double*> bufs(n, nullptr);
+    std::vector<uint8_t*> b8(n, nullptr);
+    std::vector<uint32_t*> redo(n, nullptr);  // [count, indices...] per device (ppm mode)
+    std::vector<size_t> rows(n, 0);
     std::vector<hipStream_t> streams(n, nullptr);
     std::vector<hipEvent_t> ev0(n, nullptr), ev1(n, nullptr);
+    constexpr uint32_t kRedoCap = 1u << 16;
     int rc = CRT_OK;
     for (int d = 0; d < n && rc == CRT_OK; ++d) {
         DeviceGuard g(phys(d));
+        rows[d] = count_owned(cam->image_h, rb, static_cast<uint32_t>(n), static_cast<uint32_t>(d));
+        const bool packed = ppm || d > 0;
+        const size_t px = (packed ? rows[d] : H) * W;
         if (hipStreamCreateWithFlags(&streams[d], hipStreamNonBlocking) != hipSuccess ||
-            hipMalloc(&bufs[d], frame * sizeof(double)) != hipSuccess ||
+            hipMalloc(&bufs[d], std::max<size_t>(1, px) * 3 * sizeof(double)) != hipSuccess ||
+            (ppm && hipMalloc(&b8[d], std::max<size_t>(1, px) * 3) != hipSuccess) ||
+            (ppm && hipMalloc(&redo[d], (1 + kRedoCap) * sizeof(uint32_t)) != hipSuccess) ||
             hipEventCreate(&ev0[d]) != hipSuccess || hipEventCreate(&ev1[d]) != hipSuccess) {
+            (void)hipGetLastError();
             rc = fail(CRT_E_HIP, "render: per-device setup failed on device " + std::to_string(phys(d)));
             break;
         }
-        crt_tiling t{rb, static_cast<uint32_t>(n), static_cast<uint32_t>(d), 0};
+        crt_tiling t{rb, static_cast<uint32_t>(n), static_cast<uint32_t>(d), packed ? CRT_TILING_PACKED : 0u};
         (void)hipEventRecord(ev0[d], streams[d]);
         rc = device_render(s, phys(d), cam, &t, bufs[d], streams[d], nullptr);
+        if (rc == CRT_OK && ppm && px) {
+            if (hipMemsetAsync(redo[d], 0, sizeof(uint32_t), streams[d]) != hipSuccess) {
+                rc = fail(CRT_E_HIP, "render: redo counter");
+                break;
+            }
+            hipLaunchKernelGGL(dev::ppm8_kernel, dim3(static_cast<uint32_t>((px + 255) / 256)), dim3(256), 0, streams[d],
+                               bufs[d], static_cast<uint64_t>(px), b8[d], redo[d], kRedoCap);
+            if (hipGetLastError() != hipSuccess) rc = fail(CRT_E_HIP, "render: ppm8_kernel launch");
+        }
         (void)hipEventRecord(ev1[d], streams[d]);
     }
-    // 3. gather into device 0's frame: one strided copy per device (full 4-row blocks; the frame's
-    // last block may be short and is copied on its own), then one device-to-host copy
+    // 3. gather into device 0: one strided copy per device, then one device-to-host copy
+    uint8_t* frame8 = nullptr;
+    std::vector<uint8_t> h8;
     if (rc == CRT_OK) {
         DeviceGuard g(0);
-        const size_t row_bytes = W * 3 * sizeof(double);
-        for (int d = 1; d < n && rc == CRT_OK; ++d) {
-            if (!emulate) {
-                hipError_t pe = hipDeviceEnablePeerAccess(d, 0);
-                if (pe != hipSuccess && pe != hipErrorPeerAccessAlreadyEnabled) (void)hipGetLastError();
-            }
+        if (ppm && hipMalloc(&frame8, std::max<size_t>(1, H * W * 3)) != hipSuccess) {
+            (void)hipGetLastError();
+            rc = fail(CRT_E_HIP, "render: frame buffer");
+        }
+        const size_t row_bytes = W * 3 * (ppm ? 1 : sizeof(double));
+        for (int d = ppm ? 0 : 1; d < n && rc == CRT_OK; ++d) {
+            if (!emulate && d > 0) enable_peer_once(0, d);
             if (hipStreamWaitEvent(streams[0], ev1[d], 0) != hipSuccess) {
                 rc = fail(CRT_E_HIP, "render: gather wait failed");
                 break;
             }
-            const size_t first = static_cast<size_t>(d) * rb, step = static_cast<size_t>(n) * rb;
-            if (first >= H) continue;
-            const size_t blocks = (H - first + step - 1) / step;     // blocks of device d
-            const size_t last = first + (blocks - 1) * step;         // first row of its last block
-            const size_t full = last + rb <= H ? blocks : blocks - 1; // blocks with all 4 rows
-            hipError_t e = hipSuccess;
-            if (full)
-                e = hipMemcpy2DAsync(bufs[0] + first * W * 3, step * row_bytes, bufs[d] + first * W * 3,
-                                     step * row_bytes, rb * row_bytes, full, hipMemcpyDeviceToDevice, streams[0]);
-            if (e == hipSuccess && full < blocks)
-                e = hipMemcpyAsync(bufs[0] + last * W * 3, bufs[d] + last * W * 3, (H - last) * row_bytes,
-                                   hipMemcpyDeviceToDevice, streams[0]);
+            const hipError_t e = ppm ? gather_packed(reinterpret_cast<char*>(frame8), reinterpret_cast<const char*>(b8[d]),
+                                                     H, rb, n, d, row_bytes, streams[0])
+                                     : gather_packed(reinterpret_cast<char*>(bufs[0]), reinterpret_cast<const char*>(bufs[d]),
+                                                     H, rb, n, d, row_bytes, streams[0]);
             if (e != hipSuccess) rc = fail(CRT_E_HIP, std::string("render: gather from device ") +
-                                                          std::to_string(d) + ": " + hipGetErrorString(e));
+                                                         std::to_string(d) + ": " + hipGetErrorString(e));
         }
         if (rc == CRT_OK) {
-            hipError_t e = hipMemcpyAsync(h_rgb, bufs[0], frame * sizeof(double), hipMemcpyDeviceToHost, streams[0]);
+            hipError_t e;
+            if (ppm) {
+                h8.resize(H * W * 3);
+                e = hipMemcpyAsync(h8.data(), frame8, h8.size(), hipMemcpyDeviceToHost, streams[0]);
+            } else {
+                e = hipMemcpyAsync(h_rgb, bufs[0], H * W * 3 * sizeof(double), hipMemcpyDeviceToHost, streams[0]);
+            }
             if (e == hipSuccess) e = hipStreamSynchronize(streams[0]);
             if (e != hipSuccess) rc = fail(CRT_E_HIP, std::string("render: ") + hipGetErrorString(e));
         }
@@ -2882,12 +2727,61 @@ int render_multi(crt_scene* s, const crt_camera* cam, int num_devices, double* h
         float ms = 0;
         if (rc == CRT_OK && hipEventElapsedTime(&ms, ev0[d], ev1[d]) == hipSuccess) max_ms = std::max(max_ms, ms);
     }
+    // 4. ppm mode: 8-bit values to int32, and the pixels each device left to the host
+    if (rc == CRT_OK && ppm) {
+        for (size_t i = 0; i < H * W * 3; ++i) h_ppm[i] = h8[i];
+        for (int d = 0; d < n && rc == CRT_OK; ++d) {
+            if (!rows[d]) continue;
+            DeviceGuard g(phys(d));
+            uint32_t cnt = 0;
+            if (hipMemcpy(&cnt, redo[d], sizeof cnt, hipMemcpyDeviceToHost) != hipSuccess) {
+                rc = fail(CRT_E_HIP, "render: redo count");
+                break;
+            }
+            if (!cnt) continue;
+            const size_t px = rows[d] * W;
+            std::vector<uint32_t> idx;
+            if (cnt <= kRedoCap) {  // the listed pixels
+                idx.resize(cnt);
+                if (hipMemcpy(idx.data(), redo[d] + 1, cnt * sizeof(uint32_t), hipMemcpyDeviceToHost) != hipSuccess) {
+                    rc = fail(CRT_E_HIP, "render: redo list");
+                    break;
+                }
+            }
+            std::vector<double> rgb(cnt <= kRedoCap ? 3 * idx.size() : 3 * px);
+            const bool whole = cnt > kRedoCap;  // more than the list holds: every pixel of the device
+            if (whole) {
+                if (hipMemcpy(rgb.data(), bufs[d], 3 * px * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess) rc = CRT_E_HIP;
+            } else {
+                for (size_t j = 0; j < idx.size() && rc == CRT_OK; ++j)
+                    if (hipMemcpy(rgb.data() + 3 * j, bufs[d] + 3 * static_cast<size_t>(idx[j]), 3 * sizeof(double),
+                                  hipMemcpyDeviceToHost) != hipSuccess) rc = CRT_E_HIP;
+            }
+            if (rc != CRT_OK) {
+                rc = fail(CRT_E_HIP, "render: redo pixels");
+                break;
+            }
+            const size_t m = whole ? px : idx.size();
+            for (size_t j = 0; j < m; ++j) {
+                const size_t k = whole ? j : idx[j];  // packed pixel index on device d
+                const size_t kr = k / W, col = k % W;
+                const size_t row = (kr / rb * static_cast<size_t>(n) + static_cast<size_t>(d)) * rb + kr % rb;
+                ppm_pixel_host(rgb.data() + 3 * j, h_ppm + 3 * (row * W + col));
+            }
+        }
+    }
     for (int d = 0; d < n; ++d) {
         DeviceGuard g(phys(d));
         if (bufs[d]) (void)hipFree(bufs[d]);
+        if (b8[d]) (void)hipFree(b8[d]);
+        if (redo[d]) (void)hipFree(redo[d]);
         if (streams[d]) (void)hipStreamDestroy(streams[d]);
         if (ev0[d]) (void)hipEventDestroy(ev0[d]);
         if (ev1[d]) (void)hipEventDestroy(ev1[d]);
+    }
+    if (frame8) {
+        DeviceGuard g(0);
+        (void)hipFree(frame8);
     }
     if (stats && rc == CRT_OK) {
         *stats = crt_render_stats{};
@@ -2897,20 +2791,29 @@ int render_multi(crt_scene* s, const crt_camera* cam, int num_devices, double* h
     return rc;
 }
 
+int render_multi(crt_scene* s, const crt_camera* cam, int num_devices, double* h_rgb,
+                 crt_render_stats* stats) {
+    return render_multi_impl(s, cam, num_devices, h_rgb, nullptr, stats);
+}
+
+int render_multi_ppm(crt_scene* s, const crt_camera* cam, int num_devices, int32_t* h_values,
+                     crt_render_stats* stats) {
+    return render_multi_impl(s, cam, num_devices, nullptr, h_values, stats);
+}
+
 // The compile-time switches this library was built with (bench.py hashes them with the kernel
 // sources, so a PMC summary is only used for the exact build it was collected on).
+#ifndef CRT_ARCH
+#define CRT_ARCH "unknown"
+#endif
 #define CRT_STR2(x) #x
 #define CRT_STR(x) CRT_STR2(x)
 const char* device_build_info() {
-    return "arch=gfx950 CRT_BLOCK=" CRT_STR(CRT_BLOCK) " CRT_TILE_W=" CRT_STR(CRT_TILE_W)
-           " CRT_SPEC_MASKED=" CRT_STR(CRT_SPEC_MASKED) " CRT_ACC_LDS=" CRT_STR(CRT_ACC_LDS)
-           " CRT_MANY_WAVES=" CRT_STR(CRT_MANY_WAVES) " CRT_EXACT_SHORTCUTS=" CRT_STR(CRT_EXACT_SHORTCUTS)
+    // every compile-time parameter of the kernels (the numeric tuning knobs; the library has no
+    // other build switches), and the offload target the Makefile compiled for
+    return "arch=" CRT_ARCH " CRT_BLOCK=" CRT_STR(CRT_BLOCK) " CRT_TILE_W=" CRT_STR(CRT_TILE_W)
            " CRT_WAVES_PER_EU=" CRT_STR(CRT_WAVES_PER_EU) " CRT_WAVES_PER_EU_LDS=" CRT_STR(CRT_WAVES_PER_EU_LDS)
-           " CRT_SHADE_BATCH=" CRT_STR(CRT_SHADE_BATCH) " CRT_SHADE_MIN=" CRT_STR(CRT_SHADE_MIN)
-           " CRT_PENDING_MAX=" CRT_STR(CRT_PENDING_MAX) " CRT_TOP_TREELET=" CRT_STR(CRT_TOP_TREELET)
-           " CRT_SPEC_WALK=" CRT_STR(CRT_SPEC_WALK) " CRT_COUNT_SPEC=" CRT_STR(CRT_COUNT_SPEC)
-           " CRT_PRIO_WALK=" CRT_STR(CRT_PRIO_WALK) " CRT_PRIO_LEAF=" CRT_STR(CRT_PRIO_LEAF)
-           " CRT_PRIO_SHADE=" CRT_STR(CRT_PRIO_SHADE) " CRT_CHUNK_MIN=" CRT_STR(CRT_CHUNK_MIN);
+           " CRT_SHADE_BATCH=" CRT_STR(CRT_SHADE_BATCH) " CRT_CHUNK_MIN=" CRT_STR(CRT_CHUNK_MIN);
 }
 
 }  // namespace crt

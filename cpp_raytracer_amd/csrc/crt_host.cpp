@@ -400,6 +400,9 @@ static int build_bvh(crt_scene* s, const crt_bvh_params& prm) {
                 cc[3 * i + 2] = c.z;
             }
         });
+        if (std::getenv("CRT_DEBUG_BUILD"))
+            std::fprintf(stderr, "bvh phase %-10s %8.3f ms\n", "host prep",
+                         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
         int rc = device_build_bvh(s, prm.num_buckets, prm.max_prims_in_node,
                                   static_cast<int>(prm.build_device) - 1, bx, cc);
         if (rc) return rc;
@@ -1164,6 +1167,13 @@ int crt_render(crt_scene* s, const crt_camera* cam, int num_devices, double* h_r
     clear_error();
     if (!s || !cam || !h_rgb) return fail(CRT_E_INVALID, "crt_render: null argument");
     return render_multi(s, cam, num_devices, h_rgb, stats);
+}
+
+int crt_render_ppm(crt_scene* s, const crt_camera* cam, int num_devices, int32_t* h_values,
+                   crt_render_stats* stats) {
+    clear_error();
+    if (!s || !cam || !h_values) return fail(CRT_E_INVALID, "crt_render_ppm: null argument");
+    return render_multi_ppm(s, cam, num_devices, h_values, stats);
 }
 
 int crt_ppm_values(int device, const double* d_rgb, size_t n, int32_t* h_values, void* stream) {

@@ -204,4 +204,6 @@ int device_ppm_values(int device, const double* d_rgb, size_t n, int32_t* h_valu
 void ppm_pixel_host(const double rgb[3], int32_t out[3]);
 int render_multi(crt_scene* s, const crt_camera* cam, int num_devices, double* h_rgb,
                  crt_render_stats* stats);
+int render_multi_ppm(crt_scene* s, const crt_camera* cam, int num_devices, int32_t* h_values,
+                     crt_render_stats* stats);
 }  // namespace crt

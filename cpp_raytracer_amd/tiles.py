@@ -46,8 +46,25 @@ class TileGather:
         if self.world == 1:
             return frame
         self.tile[: self.n_mine].copy_(frame.index_select(0, self.mine))
-        # one all-gather straight into the rank-major tile array (no per-rank parts + concat)
-        dist.all_gather_into_tensor(self.full, self.tile, group=self.group)
-        out = torch.empty_like(frame)
+        return self.gather_packed(self.tile)
+
+    def new_tile(self) -> torch.Tensor:
+        """A (max_rows, w, 3) tile buffer: a rank renders its rows into the first n_mine rows with
+        crt_tiling{row_block, world, rank, CRT_TILING_PACKED} (its share of the frame only)."""
+        return torch.zeros_like(self.tile)
+
+    def gather_packed(self, tile: torch.Tensor) -> torch.Tensor:
+        """tile: this rank's owned rows in order (new_tile / CRT_TILING_PACKED). Returns the
+        assembled (h, w, 3) frame on every rank: one all-gather straight into the rank-major tile
+        array (no per-rank parts + concat), then one row scatter."""
+        if tile.is_cuda and dist.get_backend(self.group) == "gloo":
+            # the one-GPU rehearsal of the N-rank path (ranks sharing a device, which RCCL
+            # refuses): gloo gathers through host memory
+            full = self.full.cpu()
+            dist.all_gather_into_tensor(full, tile.cpu(), group=self.group)
+            self.full.copy_(full)
+        else:
+            dist.all_gather_into_tensor(self.full, tile, group=self.group)
+        out = torch.empty(self.h, self.w, 3, dtype=tile.dtype, device=tile.device)
         out.index_copy_(0, self.dst, self.full.index_select(0, self.src))
         return out

@@ -113,12 +113,15 @@ typedef struct crt_camera {
 } crt_camera;
 
 /* Rows owned by one device/rank: row r is rendered iff (r / row_block) % tile_count == tile_index.
- * {1,1,0} (or NULL) = the whole frame. */
+ * {1,1,0,0} (or NULL) = the whole frame. flags: CRT_TILING_PACKED = the output buffer holds only
+ * the owned rows, packed in order (owned row k at offset k * image_w * 3): a rank or device then
+ * allocates its share of the frame, not the whole frame. */
+#define CRT_TILING_PACKED 1u
 typedef struct crt_tiling {
     uint32_t row_block;
     uint32_t tile_count;
     uint32_t tile_index;
-    uint32_t reserved;
+    uint32_t flags;
 } crt_tiling;
 
 typedef struct crt_scene crt_scene; /* opaque: flattened primitives + BVH + device copies */
@@ -216,7 +219,8 @@ void crt_scene_destroy(crt_scene* scene);
 int crt_camera_resolve(const crt_camera_settings* settings, crt_camera* out);
 
 /* Render the owned rows of the frame into d_rgb (DEVICE pointer on the scene's device,
- * image_h*image_w*3 doubles, row-major, the layout of Image::operator[] image.h:32-33).
+ * image_h*image_w*3 doubles, row-major, the layout of Image::operator[] image.h:32-33; with
+ * CRT_TILING_PACKED only owned_rows*image_w*3 doubles, the owned rows in order).
  * Enqueued on `stream`; returns without waiting. Rows not owned are left untouched.
  * Output is the per-pixel mean over samples_per_pixel samples (camera.h:285-292). */
 int crt_render_async(const crt_scene* scene, int device, const crt_camera* cam,
@@ -231,6 +235,13 @@ int crt_render_count(const crt_scene* scene, int device, const crt_camera* cam,
  * memory h_rgb. */
 int crt_render(crt_scene* scene, const crt_camera* cam, int num_devices, double* h_rgb,
                crt_render_stats* stats);
+
+/* crt_render fused with Image::send_as_ppm's integers (image.h:38-56; RGB::as_string
+ * rgb.h:99-115, the values crt_ppm_values gives): every device tone-maps its own rows to 8-bit
+ * values before the gather, so 3 bytes a pixel cross xGMI and PCIe instead of 24. h_values: host,
+ * image_w*image_h*3 int32, identical to crt_ppm_values of crt_render's frame. */
+int crt_render_ppm(crt_scene* scene, const crt_camera* cam, int num_devices, int32_t* h_values,
+                   crt_render_stats* stats);
 
 /* Closest hits of n rays (host arrays; rays[i] = {ox,oy,oz,dx,dy,dz}) against the scene on
  * `device`, time interval (t_min, t_max) exclusive, as BVH::hit_by (bvh.h:585-715). */

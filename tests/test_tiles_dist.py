@@ -37,12 +37,19 @@ def worker(rank, world, port, h, w, rb, q):
         frame[mine] = want[mine]  # "render" only the owned rows
         g = TileGather(h, w, world, rank, "cpu", row_block=rb)
         out = g.gather(frame)
-        q.put((rank, bool(torch.equal(out, want))))
+        # the packed route bench.py takes: the rank's rows only, in order (CRT_TILING_PACKED)
+        tile = g.new_tile()
+        tile[: len(mine)] = want[mine]
+        out2 = g.gather_packed(tile)
+        q.put((rank, bool(torch.equal(out, want)) and bool(torch.equal(out2, want))))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,h,w,rb", [(2, 800, 12, 16), (3, 77, 5, 16), (2, 9, 4, 16)])
+# row_block 4 is what bench.py and crt_render use (800 rows deal exactly over 1, 2, 4, 8 ranks);
+# 16 and 3 cover other block sizes and short last blocks
+@pytest.mark.parametrize("world,h,w,rb", [(2, 800, 12, 4), (3, 77, 5, 4), (2, 9, 4, 4), (4, 90, 3, 4),
+                                          (2, 800, 12, 16), (3, 77, 5, 3)])
 def test_tile_gather_assembles_frame(world, h, w, rb):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -57,7 +64,8 @@ def test_tile_gather_assembles_frame(world, h, w, rb):
     assert all(ok for _, ok in res), res
 
 
-@pytest.mark.parametrize("h,rb,world", [(800, 16, 8), (2160, 16, 8), (675, 16, 3), (5, 16, 4)])
+@pytest.mark.parametrize("h,rb,world", [(800, 4, 8), (2160, 4, 8), (1080, 4, 8), (675, 4, 3), (5, 4, 4),
+                                        (800, 16, 8), (5, 16, 4)])
 def test_row_partition_covers_every_row_once(h, rb, world):
     rows = sorted(r for k in range(world) for r in owned_rows(h, rb, world, k))
     assert rows == list(range(h))
