@@ -69,6 +69,23 @@ def kernel_source_sha() -> str:
     return h.hexdigest()[:16]
 
 
+def cgroup_cpu_quota() -> float | None:
+    """CPUs' worth of time the cgroup grants this process (cpu.max quota / period), or None."""
+    for p in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            q, per = Path(p).read_text().split()[:2]
+            if q != "max":
+                return round(int(q) / int(per), 2)
+        except (OSError, ValueError):
+            pass
+    try:
+        q = int(Path("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read_text())
+        per = int(Path("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read_text())
+        return round(q / per, 2) if q > 0 else None
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_info() -> tuple[str, int, int]:
     """(CPU model, host CPUs, CPUs this process may use)."""
     model = "unknown"
@@ -143,7 +160,7 @@ def cpu_baseline(args, scene_data, log) -> dict | None:
     ref = ROOT / "oracle" / "_ref" / "ref_driver"
     runs = max(1, args.cpu_runs)
     spp = args.cpu_spp or args.spp
-    host = {"cpu_model": model, "host_cpus": host_cpus, "usable_cpus": usable}
+    host = {"cpu_model": model, "host_cpus": host_cpus, "usable_cpus": usable, "cgroup_cpu_quota": cgroup_cpu_quota()}
 
     def frame(n_spp):
         return crt.SceneData(scene_data.materials, scene_data.objects,
@@ -177,7 +194,8 @@ def cpu_baseline(args, scene_data, log) -> dict | None:
                     r2 = ref_rates(args.cpu_share_spp, share, 1)
                     out["gpu_cpu_share"] = {"value": round(r2[0], 4), "unit": "Msamples/s", "cores": share,
                                             "sample": desc(args.cpu_share_spp, 1) + " on OMP_NUM_THREADS "
-                                            "(the GPU box's CPU share for one GPU); secondary, not the baseline"}
+                                            "(the GPU box's CPU share for one GPU); secondary, not the baseline: "
+                                            "with a cgroup quota below usable_cpus, usable_cpus threads oversubscribe it"}
                 return out
             except Exception as e:  # pragma: no cover - reported, not fatal
                 log(f"reference CPU baseline failed: {e}")

@@ -694,9 +694,72 @@ __global__ __launch_bounds__(kThreads) void big_swap(const ChunkInfo* __restrict
         }                                                                                   \
     } while (0)
 
-// Builds s->nodes / s->order on `device` for the (non-empty, non-linear) primitive list.
+// ---- device-side preparation and numbering ----------------------------------------------------
+using bvhgpu::kThreads;
+using bvhgpu::TNode;
+__global__ __launch_bounds__(kThreads) void iota_order(uint32_t* __restrict__ order, uint32_t n) {
+    const uint32_t i = blockIdx.x * kThreads + threadIdx.x;
+    if (i < n) order[i] = i;
+}
+// std::midpoint(double, double) as libstdc++ implements it (interval.h:31 Interval::mid, the
+// centroid of aabb.h:27): (a + b) / 2 when neither operand can overflow, else halving first.
+__device__ __forceinline__ double midpoint_ls(double a, double b) {
+    constexpr double lo = 2.2250738585072014e-308 * 2, hi = 1.7976931348623157e308 / 2;
+    const double aa = a < 0 ? -a : a, ab = b < 0 ? -b : b;
+    if (aa <= hi && ab <= hi) return (a + b) / 2;
+    if (aa < lo) return a + b / 2;
+    if (ab < lo) return a / 2 + b;
+    return a / 2 + b / 2;
+}
+// the primitives' centroids from their boxes (what crt_host.cpp's Builder computes)
+__global__ __launch_bounds__(kThreads) void centroids(const double* __restrict__ pb, double* __restrict__ pc, size_t n) {
+    const size_t i = static_cast<size_t>(blockIdx.x) * kThreads + threadIdx.x;
+    if (i >= n) return;
+    for (int k = 0; k < 3; ++k) pc[3 * i + k] = midpoint_ls(pb[6 * i + 2 * k], pb[6 * i + 2 * k + 1]);
+}
+// Preorder numbering (bvh.h:468-550) level by level: a level's build ids are contiguous [a, b)
+// (children are allocated while their parents' level is processed). Subtree sizes bottom-up,
+// then preorder positions top-down, then every node written at its position.
+__global__ __launch_bounds__(kThreads) void subtree_sizes(const TNode* __restrict__ t, uint32_t* __restrict__ size,
+                                                          uint32_t a, uint32_t b) {
+    const uint32_t i = a + blockIdx.x * kThreads + threadIdx.x;
+    if (i >= b) return;
+    size[i] = t[i].leaf ? 1u : 1u + size[t[i].left] + size[t[i].right];
+}
+__global__ __launch_bounds__(kThreads) void preorder_level(const TNode* __restrict__ t, const uint32_t* __restrict__ size,
+                                                           uint32_t* __restrict__ pre, uint32_t a, uint32_t b) {
+    const uint32_t i = a + blockIdx.x * kThreads + threadIdx.x;
+    if (i >= b || t[i].leaf) return;
+    pre[t[i].left] = pre[i] + 1;
+    pre[t[i].right] = pre[i] + 1 + size[t[i].left];
+}
+__global__ __launch_bounds__(kThreads) void emit_preorder(const TNode* __restrict__ t, const uint32_t* __restrict__ pre,
+                                                          uint32_t n, crt_bvh_node* __restrict__ out,
+                                                          uint32_t* __restrict__ max_leaf) {
+    const uint32_t i = blockIdx.x * kThreads + threadIdx.x;
+    if (i >= n) return;
+    const TNode& x = t[i];
+    crt_bvh_node o;
+    for (int q = 0; q < 6; ++q) o.bounds[q] = x.b[q];
+    o.flags = 0;
+    if (x.leaf) {
+        o.index = x.lo;
+        o.count = x.count;
+        o.axis = 0;
+        atomicMax(max_leaf, x.count);
+    } else {
+        o.index = pre[x.right];
+        o.count = 0;
+        o.axis = x.axis;
+    }
+    out[pre[i]] = o;
+}
+
+// Builds s->nodes / s->order on `device` for the (non-empty, non-linear) primitive list, from the
+// primitives' boxes (6 doubles each, in primitive order); centroids, the tree and its preorder
+// numbering are computed on the device.
 int device_build_bvh(crt_scene* s, uint32_t num_buckets, uint32_t max_leaf, int device,
-                     const std::vector<double>& boxes, const std::vector<double>& cents) {
+                     const std::vector<double>& boxes) {
     using namespace bvhgpu;
     if (num_buckets < 2 || num_buckets > kMaxBuckets)
         return fail(CRT_E_INVALID, "GPU BVH build supports 2..64 buckets");
@@ -719,9 +782,11 @@ int device_build_bvh(crt_scene* s, uint32_t num_buckets, uint32_t max_leaf, int 
     double* d_chunk_red = nullptr;
     unsigned int* d_bn = nullptr;
     unsigned long long* d_bb = nullptr;
-    std::vector<TNode> tn;
     std::vector<uint32_t> order(n);
     uint32_t nnodes = 0;
+    std::vector<uint32_t> level_end;  // build ids [level_end[L - 1], level_end[L]) are level L
+    uint32_t *d_size = nullptr, *d_pre = nullptr, *d_maxleaf = nullptr;
+    crt_bvh_node* d_out = nullptr;
     const bool dbg = std::getenv("CRT_DEBUG_BUILD") != nullptr;
     auto tp = std::chrono::steady_clock::now();
     auto phase = [&](const char* what) {  // CRT_DEBUG_BUILD: where the build's time goes
@@ -732,7 +797,6 @@ int device_build_bvh(crt_scene* s, uint32_t num_buckets, uint32_t max_leaf, int 
         tp = now;
     };
     {
-        for (size_t i = 0; i < n; ++i) order[i] = static_cast<uint32_t>(i);
         BV_TRY(hipMalloc(&d_pb, n * 6 * sizeof(double)));
         BV_TRY(hipMalloc(&d_pc, n * 3 * sizeof(double)));
         BV_TRY(hipMalloc(&d_order, n * 4));
@@ -753,8 +817,11 @@ int device_build_bvh(crt_scene* s, uint32_t num_buckets, uint32_t max_leaf, int 
         BV_TRY(hipMalloc(&d_bb, max_big * 3 * kMaxBuckets * 6 * sizeof(unsigned long long)));
         phase("alloc");
         BV_TRY(hipMemcpy(d_pb, boxes.data(), n * 6 * sizeof(double), hipMemcpyHostToDevice));
-        BV_TRY(hipMemcpy(d_pc, cents.data(), n * 3 * sizeof(double), hipMemcpyHostToDevice));
-        BV_TRY(hipMemcpy(d_order, order.data(), n * 4, hipMemcpyHostToDevice));
+        hipLaunchKernelGGL(centroids, dim3(static_cast<uint32_t>((n + kThreads - 1) / kThreads)), dim3(kThreads), 0, 0,
+                           d_pb, d_pc, n);
+        hipLaunchKernelGGL(iota_order, dim3(static_cast<uint32_t>((n + kThreads - 1) / kThreads)), dim3(kThreads), 0, 0,
+                           d_order, static_cast<uint32_t>(n));
+        BV_TRY(hipGetLastError());
         // counters: [0] nodes allocated, [1] next small tasks, [2] next big tasks
         uint32_t ctr[3] = {1, 0, 0};
         uint32_t nsmall = 0, nbig = 0;
@@ -770,6 +837,7 @@ int device_build_bvh(crt_scene* s, uint32_t num_buckets, uint32_t max_leaf, int 
         BV_TRY(hipMemcpy(d_ctr, ctr, sizeof ctr, hipMemcpyHostToDevice));
         const Params P{num_buckets, max_leaf};
         phase("upload");
+        level_end.push_back(1);  // level 1: the root
         auto tl = std::chrono::steady_clock::now();
         int level = 0;
         std::vector<ChunkInfo> chunks;
@@ -813,6 +881,7 @@ int device_build_bvh(crt_scene* s, uint32_t num_buckets, uint32_t max_leaf, int 
                 tl = now;
             }
             ++level;
+            if (ctr[0] > level_end.back()) level_end.push_back(ctr[0]);
             nsmall = ctr[1];
             nbig = ctr[2];
             if (nbig) {
@@ -825,41 +894,33 @@ int device_build_bvh(crt_scene* s, uint32_t num_buckets, uint32_t max_leaf, int 
         }
         phase("levels");
         nnodes = ctr[0];
-        tn.resize(nnodes);
-        BV_TRY(hipMemcpy(tn.data(), d_nodes, nnodes * sizeof(TNode), hipMemcpyDeviceToHost));
-        BV_TRY(hipMemcpy(order.data(), d_order, n * 4, hipMemcpyDeviceToHost));
-    }
-    phase("download");
-    {
-        // preorder numbering (bvh.h:468-550): children have larger build ids than parents
-        std::vector<uint32_t> size(nnodes, 1), pre(nnodes, 0), lvl(nnodes, 1);
-        for (size_t i = nnodes; i-- > 0;)
-            if (!tn[i].leaf) size[i] = 1 + size[tn[i].left] + size[tn[i].right];
-        s->nodes.assign(nnodes, crt_bvh_node{});
-        s->depth = 0;
-        s->max_leaf = 0;
-        for (size_t i = 0; i < nnodes; ++i) {
-            const TNode& t = tn[i];
-            crt_bvh_node& o = s->nodes[pre[i]];
-            std::memcpy(o.bounds, t.b, sizeof o.bounds);
-            s->depth = std::max(s->depth, lvl[i]);
-            if (t.leaf) {
-                o.index = t.lo;
-                o.count = t.count;
-                o.axis = 0;
-                s->max_leaf = std::max(s->max_leaf, t.count);
-            } else {
-                pre[t.left] = pre[i] + 1;
-                pre[t.right] = pre[i] + 1 + size[t.left];
-                lvl[t.left] = lvl[t.right] = lvl[i] + 1;
-                o.index = pre[t.right];
-                o.count = 0;
-                o.axis = t.axis;
-            }
+        // preorder numbering on the device: sizes bottom-up, positions top-down, then the nodes
+        BV_TRY(hipMalloc(&d_size, nnodes * 4));
+        BV_TRY(hipMalloc(&d_pre, nnodes * 4));
+        BV_TRY(hipMalloc(&d_maxleaf, 4));
+        BV_TRY(hipMalloc(&d_out, nnodes * sizeof(crt_bvh_node)));
+        BV_TRY(hipMemset(d_pre, 0, 4));
+        BV_TRY(hipMemset(d_maxleaf, 0, 4));
+        const size_t nl = level_end.size();
+        auto grid = [](uint32_t a, uint32_t b) { return dim3((b - a + kThreads - 1) / kThreads); };
+        for (size_t L = nl; L-- > 0;) {
+            const uint32_t a = L ? level_end[L - 1] : 0, b = level_end[L];
+            hipLaunchKernelGGL(subtree_sizes, grid(a, b), dim3(kThreads), 0, 0, d_nodes, d_size, a, b);
         }
+        for (size_t L = 0; L + 1 < nl; ++L) {
+            const uint32_t a = L ? level_end[L - 1] : 0, b = level_end[L];
+            hipLaunchKernelGGL(preorder_level, grid(a, b), dim3(kThreads), 0, 0, d_nodes, d_size, d_pre, a, b);
+        }
+        hipLaunchKernelGGL(emit_preorder, grid(0, nnodes), dim3(kThreads), 0, 0, d_nodes, d_pre, nnodes, d_out, d_maxleaf);
+        BV_TRY(hipGetLastError());
+        s->nodes.resize(nnodes);
+        BV_TRY(hipMemcpy(s->nodes.data(), d_out, nnodes * sizeof(crt_bvh_node), hipMemcpyDeviceToHost));
+        BV_TRY(hipMemcpy(order.data(), d_order, n * 4, hipMemcpyDeviceToHost));
+        BV_TRY(hipMemcpy(&s->max_leaf, d_maxleaf, 4, hipMemcpyDeviceToHost));
+        s->depth = static_cast<uint32_t>(nl);
         s->order = std::move(order);
     }
-    phase("preorder");
+    phase("preorder + download");
 done:
     (void)hipFree(d_pb);
     (void)hipFree(d_pc);
@@ -878,6 +939,10 @@ done:
     (void)hipFree(d_chunk_red);
     (void)hipFree(d_bn);
     (void)hipFree(d_bb);
+    (void)hipFree(d_size);
+    (void)hipFree(d_pre);
+    (void)hipFree(d_maxleaf);
+    (void)hipFree(d_out);
     (void)hipSetDevice(prev);
     return rc;
 }

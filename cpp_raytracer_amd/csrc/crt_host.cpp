@@ -5,6 +5,7 @@
 // compiled with -ffp-contract=off) so the BVH node arrays and camera vectors are bit-identical
 // to the ones the reference computes. Citations are paths in DeltaPavonis/cpp_raytracer.
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdint>
@@ -193,7 +194,7 @@ static void emit_object(const crt_object& o, Prim* out) {
     }
 }
 
-static int flatten(crt_scene* s) {
+static int flatten(crt_scene* s, bool boxes) {
     // validate in object order (first error wins), then emit in parallel at prefix offsets
     const size_t no = s->objects.size();
     std::vector<size_t> off(no + 1, 0);
@@ -213,9 +214,25 @@ static int flatten(crt_scene* s) {
             return fail(CRT_E_INVALID, "material " + std::to_string(i) + " has unknown kind");
     }
     s->prims.resize(off[no]);
+    // boxes: the GPU BVH build's input, written while the primitives are hot in cache
+    if (boxes) s->pbox.resize(off[no] * 6);
+    std::atomic<bool> nan_box{false};
     parallel_for(no, 4096, [&](size_t a, size_t b) {
-        for (size_t i = a; i < b; ++i) emit_object(s->objects[i], s->prims.data() + off[i]);
+        bool nan = false;
+        for (size_t i = a; i < b; ++i) {
+            Prim* p = s->prims.data() + off[i];
+            emit_object(s->objects[i], p);
+            if (boxes)
+                for (size_t j = off[i]; j < off[i + 1]; ++j, ++p) {
+                    std::memcpy(&s->pbox[6 * j], p->box, 6 * sizeof(double));
+                    for (int k = 0; k < 6; ++k) nan = nan || std::isnan(p->box[k]);
+                }
+        }
+        if (nan) nan_box = true;
     });
+    // the GPU build reproduces the host fold only for NaN-free boxes (with a NaN, fmin/fmax pick
+    // by operand order in ways its order-preserving keys do not model): such scenes build on the host
+    if (nan_box) std::vector<double>().swap(s->pbox);
     return CRT_OK;
 }
 
@@ -354,15 +371,6 @@ void flatten_tree(const TreeNode* t, std::vector<crt_bvh_node>& out, size_t& nex
 }
 }  // namespace
 
-// The GPU build reproduces the host fold only for NaN-free boxes (with a NaN, fmin/fmax pick by
-// operand order in ways the order-preserving keys do not model); those scenes build on the host.
-static bool gpu_buildable(const std::vector<Prim>& prims) {
-    for (const Prim& p : prims)
-        for (double v : p.box)
-            if (std::isnan(v)) return false;
-    return true;
-}
-
 static int build_bvh(crt_scene* s, const crt_bvh_params& prm) {
     auto t0 = std::chrono::steady_clock::now();
     const size_t n = s->prims.size();
@@ -388,23 +396,12 @@ static int build_bvh(crt_scene* s, const crt_bvh_params& prm) {
         s->nodes.push_back(e);
         s->depth = 1;
         s->max_leaf = static_cast<uint32_t>(n);
-    } else if (prm.build_device != 0 && gpu_buildable(s->prims)) {
-        // the same tree built on a GPU (crt_bvh_gpu.hip); boxes and centroids as Builder's
-        std::vector<double> bx(n * 6), cc(n * 3);
-        parallel_for(n, 8192, [&](size_t a, size_t b) {
-            for (size_t i = a; i < b; ++i) {
-                std::memcpy(&bx[6 * i], s->prims[i].box, 6 * sizeof(double));
-                const V3 c = box_of(s->prims[i].box).centroid();
-                cc[3 * i] = c.x;
-                cc[3 * i + 1] = c.y;
-                cc[3 * i + 2] = c.z;
-            }
-        });
-        if (std::getenv("CRT_DEBUG_BUILD"))
-            std::fprintf(stderr, "bvh phase %-10s %8.3f ms\n", "host prep",
-                         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+    } else if (prm.build_device != 0 && !s->pbox.empty()) {
+        // the same tree built on a GPU (crt_bvh_gpu.hip) from the boxes flatten() wrote; the
+        // centroids are computed there (Builder's box_of(...).centroid())
         int rc = device_build_bvh(s, prm.num_buckets, prm.max_prims_in_node,
-                                  static_cast<int>(prm.build_device) - 1, bx, cc);
+                                  static_cast<int>(prm.build_device) - 1, s->pbox);
+        std::vector<double>().swap(s->pbox);
         if (rc) return rc;
     } else {
         if (prm.num_buckets < 2) return fail(CRT_E_INVALID, "num_buckets must be >= 2");
@@ -414,6 +411,7 @@ static int build_bvh(crt_scene* s, const crt_bvh_params& prm) {
         size_t next = 0;
         flatten_tree(root.get(), s->nodes, next, 1, s->depth, s->max_leaf);
     }
+    std::vector<double>().swap(s->pbox);
     s->build_ms =
         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return CRT_OK;
@@ -1080,7 +1078,7 @@ int crt_scene_create(const crt_material* materials, size_t num_materials,
         s = std::make_unique<crt_scene>();
         s->materials.assign(materials, materials + num_materials);
         s->objects.assign(objects, objects + num_objects);
-        int rc = flatten(s.get());
+        int rc = flatten(s.get(), prm.build_device != 0 && prm.linear == 0);
         if (rc) return rc;
         if (s->prims.size() >= 0x7fffffffu) return fail(CRT_E_INVALID, "too many primitives");
         s->linear = prm.linear != 0;

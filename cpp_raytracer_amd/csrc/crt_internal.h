@@ -137,6 +137,7 @@ struct crt_scene {
     std::vector<crt_material> materials;
     std::vector<crt_object> objects;
     std::vector<crt::Prim> prims;
+    std::vector<double> pbox;              // primitive boxes, 6 doubles each (GPU BVH build only)
     std::vector<crt_bvh_node> nodes;
     std::vector<uint32_t> order;           // slot -> primitive index
     // device-layout staging (host)
@@ -198,7 +199,7 @@ int device_count(int* n);
 const char* device_build_info();
 int device_guard(crt_scene* s, int device, uint64_t* schlick_undecided, bool reset);
 int device_build_bvh(crt_scene* s, uint32_t num_buckets, uint32_t max_leaf, int device,
-                     const std::vector<double>& boxes, const std::vector<double>& cents);
+                     const std::vector<double>& boxes);
 int device_ppm_values(int device, const double* d_rgb, size_t n, int32_t* h_values, void* stream);
 // host: RGB::as_string's three integers for one pixel (std::pow, x86 int conversion)
 void ppm_pixel_host(const double rgb[3], int32_t out[3]);

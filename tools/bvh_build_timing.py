@@ -1,7 +1,23 @@
-import time, os, sys
-sys.path.insert(0, os.environ.get("GRAFT_REPO_ROOT", "/root/repo"))
-import cpp_raytracer_amd as crt
+"""Where the millions-of-spheres scene's set-up time goes (BASELINE config 4: 2,106,105 spheres):
+scene creation with the GPU BVH build (crt_scene_create with build_device; build_ms = the BVH
+build alone, host preparation included), then the upload (stage_image + the copy to HBM).
+CRT_DEBUG_BUILD=1 also prints the GPU build's phases. usage: python tools/bvh_build_timing.py [reps]"""
+import os
+import sys
+import time
+
+sys.path.insert(0, os.environ.get("GRAFT_REPO_ROOT", os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+import cpp_raytracer_amd as crt  # noqa: E402
+
+reps = int(sys.argv[1]) if len(sys.argv) > 1 else 3
 d = crt.SceneData.named("millions", 42)
-crt.GpuScene(crt.SceneData.named("config1"), build_device=0)  # warm up HIP
-t = time.perf_counter(); g = crt.GpuScene(d, build_device=0); t1 = time.perf_counter()
-print("gpu build total ms", (t1 - t) * 1e3, "reported", g.info().build_ms)
+crt.GpuScene(crt.SceneData.named("config1"), build_device=0).upload(0)  # warm up HIP
+for r in range(reps):
+    t0 = time.perf_counter()
+    g = crt.GpuScene(d, build_device=0)
+    t1 = time.perf_counter()
+    g.upload(0)
+    t2 = time.perf_counter()
+    print(f"rep {r}: scene create {(t1 - t0) * 1e3:.1f} ms (build_ms {g.info().build_ms:.1f}), "
+          f"upload {(t2 - t1) * 1e3:.1f} ms, total {(t2 - t0) * 1e3:.1f} ms", flush=True)
+    g.close()
