@@ -759,7 +759,7 @@ __global__ __launch_bounds__(kThreads) void emit_preorder(const TNode* __restric
 // primitives' boxes (6 doubles each, in primitive order); centroids, the tree and its preorder
 // numbering are computed on the device.
 int device_build_bvh(crt_scene* s, uint32_t num_buckets, uint32_t max_leaf, int device,
-                     const std::vector<double>& boxes) {
+                     const BigVec<double>& boxes) {
     using namespace bvhgpu;
     if (num_buckets < 2 || num_buckets > kMaxBuckets)
         return fail(CRT_E_INVALID, "GPU BVH build supports 2..64 buckets");
@@ -782,7 +782,7 @@ int device_build_bvh(crt_scene* s, uint32_t num_buckets, uint32_t max_leaf, int 
     double* d_chunk_red = nullptr;
     unsigned int* d_bn = nullptr;
     unsigned long long* d_bb = nullptr;
-    std::vector<uint32_t> order(n);
+    BigVec<uint32_t> order(n);
     uint32_t nnodes = 0;
     std::vector<uint32_t> level_end;  // build ids [level_end[L - 1], level_end[L]) are level L
     uint32_t *d_size = nullptr, *d_pre = nullptr, *d_maxleaf = nullptr;

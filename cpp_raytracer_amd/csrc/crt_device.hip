@@ -12,6 +12,7 @@
 #define CRT_HD __host__ __device__ __forceinline__
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -120,7 +121,6 @@ struct Work {
     uint32_t sentinel;      // the sentinel node's reference (byte offset into the f32 nodes)
     uint32_t lds_cam;       // LDS copy of the CamView (read where used: keeps it out of SGPRs)
     uint32_t lds_acc;       // five-wave instances: the lanes' pixel sums (3 x kBlock doubles)
-    uint32_t lds_pool;      // render_pool_kernel: the ray-exchange rings
     uint32_t packed;        // the output holds only the owned rows (CRT_TILING_PACKED)
     // instrumented pass only (COUNT): walk speculatively like the timed kernel (CRT_COUNT_SPEC=1),
     // count per-round lane numbers (CRT_ROUND_COUNTERS=1; their atomics shift the phase timings)
@@ -1123,14 +1123,22 @@ __device__ __forceinline__ void leaf_step(const SceneView& S, Stack<SE>& st, con
         leaf_ray32(o, d, R.a, tmin, R.tmax, L);
         uint32_t cand = 0;
         const uint32_t nbits = (range.y + 1) & ~1u;
-        for (uint32_t i = 0; i < range.y; i += 2) {
-            if (COUNT) {
-                ctr.sphere_tests += i + 1 < range.y ? 2 : 1;
-                if (wave_leader()) ctr.it_leaf += 2;
+        if constexpr (LS) {
+            for (uint32_t i = 0; i < range.y; i += 2) {
+                if (COUNT) {
+                    ctr.sphere_tests += i + 1 < range.y ? 2 : 1;
+                    if (wave_leader()) ctr.it_leaf += 2;
+                }
+                cand = sphere_pair_candidates(cand, pair_at((LdsPair*)static_cast<uintptr_t>(S.spair_lds + ((range.x + i) << 5))), L);
             }
-            const DevSpherePair rec = LS ? pair_at((LdsPair*)static_cast<uintptr_t>(S.spair_lds + ((range.x + i) << 5)))
-                                         : pair_at((GlobalPair*)(S.spair + range.x + i));
-            cand = sphere_pair_candidates(cand, rec, L);
+        } else {
+            for (uint32_t i = 0; i < range.y; i += 2) {
+                if (COUNT) {
+                    ctr.sphere_tests += i + 1 < range.y ? 2 : 1;
+                    if (wave_leader()) ctr.it_leaf += 2;
+                }
+                cand = sphere_pair_candidates(cand, pair_at((GlobalPair*)(S.spair + range.x + i)), L);
+            }
         }
         cand &= ~(range.y & 1u);  // an odd count's last verdict is the slot after the leaf
         while (cand) {
@@ -1763,490 +1771,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W5 ? kMa
     }
 }
 
-// ---- block-level ray exchange (north_star: compaction of live rays between bounces) ---------
-// render_pool_kernel: the same per-lane state machine as render_kernel, but the 16 waves of a
-// 1024-thread block (one block per CU, one copy of the scene in its LDS) exchange rays through two
-// rings in LDS at every bounce boundary, so that a wave's lanes are not held by rays that wait:
-//   DONE  - rays whose closest-hit query is finished (camera.h:215: the hit record), to be shaded;
-//   FRESH - rays ready to traverse (after shading and the traversal set-up).
-// A wave traces (walk + leaf rounds, bvh.h:617-712) while it has rays to trace: after every round
-// its finished rays go to DONE and its empty lanes take FRESH rays, so the traversal rounds run
-// with every lane busy as long as FRESH holds rays. When at least kShadeBatch of its lanes hold
-// no ray to trace it shades: empty lanes take DONE rays, and lanes still empty draw new units
-// from the work queue; after the scatter (material.h:64-263) and the traversal set-up it may
-// export its fresh rays to FRESH and take DONE rays again (shading a whole batch of other waves'
-// rays), while DONE holds enough of them and FRESH is below kFreshTarget.
-// A ray carries its whole path state (origin, direction, throughput, RNG, depth, its unit's
-// pixel / sample / running sum), so any lane of the block may continue it: each sample's path is
-// the same sequence of operations whichever lanes run it, and a unit's sum is still added in
-// sample order (its next sample starts only when its path ends), so frames are bit-identical to
-// render_kernel's. No wave ever waits for another: every exchange takes what a ring holds (or has
-// room for) at that moment; the only wait is for the few LDS writes of a slot another wave has
-// already reserved (its flag), and a wave ends when its lanes, the work queue and both rings are
-// empty.
-constexpr int kPoolBlock = 1024;
-constexpr uint32_t kRingCapD = 256, kRingCapF = 256;  // powers of two
-constexpr uint32_t kDoneChunks = 8, kFreshChunks = 10;  // 16-byte chunks of a record
-constexpr uint32_t kFreshTarget = 128, kImportMin = 16, kMaxShadeIters = 4;
-// ring control: [free, full, head, tail] u32; flags[cap] u32: a bounded multi-producer /
-// multi-consumer ring with a sequence word per slot (Vyukov): slot i holds seq = t when it is
-// free for the producer of ticket t (initially t = i), t + 1 once that record is written, and
-// t + cap once its consumer has read it (free for ticket t + cap). The counters only say how many
-// a wave may take without waiting: free (room to produce) and full (records written). Tickets
-// are taken in order (tail / head), so every wait is for a ticket below one the waiter holds, on
-// a wave already past its own reservation: no cycle. data: chunk c of slot i at (c * cap + i) * 16
-// (a wave's consecutive slots are consecutive 16-byte lines: no bank conflicts).
-struct RingView {
-    uint32_t ctrl, flags, data, cap;
-};
-typedef __attribute__((address_space(3))) uint32_t LdsU32;
-typedef __attribute__((address_space(3))) Uvec4 LdsUvec4;
-__device__ __forceinline__ LdsU32* lds_u32p(uint32_t off) { return (LdsU32*)static_cast<uintptr_t>(off); }
-__device__ __forceinline__ void put16(const RingView& r, uint32_t c, uint32_t slot, Uvec4 v) {
-    *(LdsUvec4*)static_cast<uintptr_t>(r.data + (c * r.cap + slot) * 16) = v;
-}
-__device__ __forceinline__ Uvec4 get16(const RingView& r, uint32_t c, uint32_t slot) {
-    return *(LdsUvec4*)static_cast<uintptr_t>(r.data + (c * r.cap + slot) * 16);
-}
-__device__ __forceinline__ uint32_t lo32(double x) { return static_cast<uint32_t>(__double_as_longlong(x)); }
-__device__ __forceinline__ uint32_t hi32(double x) { return static_cast<uint32_t>(static_cast<uint64_t>(__double_as_longlong(x)) >> 32); }
-__device__ __forceinline__ double dbl(uint32_t lo, uint32_t hi) { return __hiloint2double(static_cast<int>(hi), static_cast<int>(lo)); }
-__device__ __forceinline__ Uvec4 pack2d(double a, double b) { return Uvec4{lo32(a), hi32(a), lo32(b), hi32(b)}; }
-__device__ __forceinline__ uint32_t rank_in(uint64_t m) {
-    return __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32), __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0u));
-}
-// Takes up to `want` from the counter at ctrl + which (free: room to produce; full: records to
-// consume) with one compare-and-swap loop of the wave's first active lane; the other lanes get the
-// count and, for the ticket counter at ctrl + tick (tail / head), the first ticket.
-__device__ __forceinline__ uint32_t ring_take(const RingView& r, uint32_t which, uint32_t tick, uint32_t want,
-                                              uint32_t& first) {
-    const uint32_t leader = static_cast<uint32_t>(__ffsll(static_cast<long long>(__ballot(1))) - 1);
-    uint32_t k = 0, t = 0;
-    if ((threadIdx.x & 63) == leader && want) {
-        LdsU32* cnt = lds_u32p(r.ctrl + which * 4);
-        uint32_t have = __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        while (true) {
-            k = min(want, have);
-            if (k == 0) break;
-            if (__hip_atomic_compare_exchange_strong(cnt, &have, have - k, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_WORKGROUP))
-                break;
-        }
-        if (k) t = __hip_atomic_fetch_add(lds_u32p(r.ctrl + tick * 4), k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-    k = __builtin_amdgcn_readlane(k, leader);
-    first = __builtin_amdgcn_readlane(t, leader);
-    return k;
-}
-__device__ __forceinline__ uint32_t ring_count(const RingView& r, uint32_t which) {
-    return __hip_atomic_load(lds_u32p(r.ctrl + which * 4), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ void ring_add(const RingView& r, uint32_t which, uint32_t k) {
-    const uint32_t leader = static_cast<uint32_t>(__ffsll(static_cast<long long>(__ballot(1))) - 1);
-    if ((threadIdx.x & 63) == leader)
-        __hip_atomic_fetch_add(lds_u32p(r.ctrl + which * 4), k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-// producers: wait until the slot is free for this ticket (its previous record has been read)
-__device__ __forceinline__ void ring_slot_free(const RingView& r, bool mine, uint32_t ticket) {
-    if (mine) {
-        LdsU32* f = lds_u32p(r.flags + (ticket & (r.cap - 1)) * 4);
-        while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != ticket) __builtin_amdgcn_s_sleep(1);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-}
-// producers: after the records are written, the flags (release), then `full`
-__device__ __forceinline__ void ring_publish(const RingView& r, bool mine, uint32_t ticket, uint32_t k) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    if (mine) __hip_atomic_store(lds_u32p(r.flags + (ticket & (r.cap - 1)) * 4), ticket + 1, __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_WORKGROUP);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    ring_add(r, 1, k);
-}
-// consumers: wait for the slot's flag (a producer that reserved it is writing it now), acquire
-__device__ __forceinline__ void ring_wait(const RingView& r, bool mine, uint32_t ticket) {
-    if (mine) {
-        LdsU32* f = lds_u32p(r.flags + (ticket & (r.cap - 1)) * 4);
-        while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != ticket + 1) __builtin_amdgcn_s_sleep(1);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-}
-// consumers: the records are read (their loads completed), each slot is free for the ticket one
-// lap later, and the room goes back to producers
-__device__ __forceinline__ void ring_release(const RingView& r, bool mine, uint32_t ticket, uint32_t k) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    if (mine) __hip_atomic_store(lds_u32p(r.flags + (ticket & (r.cap - 1)) * 4), ticket + r.cap, __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_WORKGROUP);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    ring_add(r, 0, k);
-}
-
-template <typename SE, int PM, bool COUNT>
-__global__ __launch_bounds__(kPoolBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) void render_pool_kernel(
-    SceneView Sg, CamView C, Work W, double* __restrict__ partial, Counters* __restrict__ counters) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    constexpr bool kSphOnly = PM == 0, kFlatOnly = PM == 2;
-    constexpr bool kFast = kSphOnly;  // exact sqrt / reciprocal shortcuts (sqrt_exact, recip_exact)
-    SceneView S = Sg;
-    if (static_cast<uint32_t>(reinterpret_cast<uintptr_t>((LdsByte*)smem)) != 0) __builtin_trap();
-    auto stage = [&](unsigned char* dst, const void* src, uint32_t bytes) {
-        const uint4* s4 = static_cast<const uint4*>(src);
-        uint4* d4 = reinterpret_cast<uint4*>(dst);
-        for (uint32_t i = threadIdx.x; i < bytes / 16; i += kPoolBlock) d4[i] = s4[i];
-    };
-    stage(smem, Sg.fnodes, W.bytes_nodes);
-    stage(smem + W.lds_quads, Sg.quads, W.bytes_quads);
-    S.quads = reinterpret_cast<const DevQuad*>(smem + W.lds_quads);
-    S.quads_lds = W.lds_quads;
-    if (W.quads_f32) {
-        stage(smem + W.lds_quadf, W.quads_flat ? static_cast<const void*>(Sg.quadbox) : Sg.quadf, W.bytes_quadf);
-        S.quadf_lds = W.lds_quadf;
-    }
-    S.refs_lds = W.lds_refs;
-    S.spheres_lds = W.spheres_f32 ? (W.bytes_sph64 ? W.lds_sph64 : ~0u) : W.lds_spheres;
-    if (W.spheres_f32) {
-        stage(smem + W.lds_spheres, Sg.spair, W.bytes_spheres);
-        if (W.bytes_sph64) stage(smem + W.lds_sph64, Sg.spheres, W.bytes_sph64);
-        S.spair_lds = W.lds_spheres;
-    } else {
-        stage(smem + W.lds_refs, Sg.refs, W.bytes_refs);
-        stage(smem + W.lds_spheres, Sg.spheres, W.bytes_spheres);
-        S.refs = reinterpret_cast<const uint32_t*>(smem + W.lds_refs);
-        S.spheres = reinterpret_cast<const DevSphere*>(smem + W.lds_spheres);
-    }
-    // the rings: D (done rays) then F (fresh rays), each [ctrl 16 B][flags][data]
-    const RingView RD{W.lds_pool, W.lds_pool + 16, W.lds_pool + 16 + kRingCapD * 4, kRingCapD};
-    const uint32_t f0 = RD.data + kDoneChunks * kRingCapD * 16;
-    const RingView RF{f0, f0 + 16, f0 + 16 + kRingCapF * 4, kRingCapF};
-    if (threadIdx.x < 4) {
-        *lds_u32p(RD.ctrl + threadIdx.x * 4) = threadIdx.x == 0 ? kRingCapD : 0u;
-        *lds_u32p(RF.ctrl + threadIdx.x * 4) = threadIdx.x == 0 ? kRingCapF : 0u;
-    }
-    for (uint32_t i = threadIdx.x; i < kRingCapD; i += kPoolBlock) *lds_u32p(RD.flags + i * 4) = i;
-    for (uint32_t i = threadIdx.x; i < kRingCapF; i += kPoolBlock) *lds_u32p(RF.flags + i * 4) = i;
-    if (threadIdx.x == 0) *reinterpret_cast<CamView*>(smem + W.lds_cam) = C;
-    __syncthreads();
-    const CamView& CL = *reinterpret_cast<const CamView*>(smem + W.lds_cam);
-    const float tmin32 = W.tmin32;
-    const uint32_t lane = threadIdx.x & 63;
-    LaneCounters ctr{};
-    const unsigned long long t_start = COUNT ? wall_clock64() : 0;
-    Stack<SE> st;
-    st.base = reinterpret_cast<SE*>(smem + W.lds_stack) + threadIdx.x;
-    st.stride = kPoolBlock;
-    st.base[-static_cast<ptrdiff_t>(st.stride)] = static_cast<SE>(W.sentinel);
-    uint32_t item_pos = 0, item_units = 0, item_txy = 0, item_chunk = 0;
-    bool dry = false;  // this wave found the work queue dry
-    uint32_t u_txy = 0, u_cp = 0, s = 0;
-    double acc[3] = {0, 0, 0};
-    Path P;
-    Trav R;
-    R.state = kIdle;  // kIdle: the lane holds no ray (and no unit)
-    bool shading = false;
-    uint32_t shade_iters = 0;
-    uint32_t cw = 0, cl = 0, cs = 0, cd = 0, ci = 0;
-    while (true) {
-        if (!shading) {
-            // ---- a traversal round of the lanes with a ray to trace --------------------------
-            if (__ballot(R.state == kWalk || R.state == kLeaf) != 0) {
-                if (COUNT) cw -= static_cast<uint32_t>(wall_clock64());
-                set_prio<kPrioWalk>();
-                if (!W.exact_slab && __ballot(R.state == kWalk && (R.neg & kZeroDir)) == 0) {
-                    if (R.state == kWalk) {
-                        if (!COUNT || W.count_spec)
-                            walk<SE, COUNT, false, false, true, false, true>(S, st, P.o, P.d, C.t_min, tmin32, R, ctr);
-                        else
-                            walk<SE, COUNT, false, false, true, false, false>(S, st, P.o, P.d, C.t_min, tmin32, R, ctr);
-                    }
-                } else {
-                    if (R.state == kWalk) walk<SE, COUNT, true, false, true, false, false>(S, st, P.o, P.d, C.t_min, tmin32, R, ctr);
-                }
-                if (COUNT) {
-                    const uint32_t now = static_cast<uint32_t>(wall_clock64());
-                    cw += now;
-                    cl -= now;
-                }
-                set_prio<kPrioLeaf>();
-                if (R.state == kLeaf) leaf_step<SE, COUNT, false, true, kFast>(S, st, P.o, P.d, C.t_min, tmin32, kSphOnly, !kFlatOnly && W.spheres_f32 != 0, kFlatOnly, kFlatOnly, R, ctr);
-                if (COUNT) cl += static_cast<uint32_t>(wall_clock64());
-            }
-            if (COUNT) cd -= static_cast<uint32_t>(wall_clock64());
-            set_prio<kPrioInit>();
-            // ---- finished rays to DONE, as many as FRESH can replace (a swap: no lane is left
-            // empty while rays wait to be traced) ------------------------------------------------
-            {
-                const uint64_t m = __ballot(R.state == kDone);
-                const uint32_t nf = m ? ring_count(RF, 1) : 0u;
-                if (m && nf) {
-                    uint32_t t0;
-                    const uint32_t k = ring_take(RD, 0, 3, min(static_cast<uint32_t>(__popcll(m)), nf), t0);
-                    const uint32_t r = rank_in(m);
-                    const bool mine = R.state == kDone && r < k;
-                    const uint32_t ticket = t0 + r, slot = ticket & (kRingCapD - 1);
-                    if (k) ring_slot_free(RD, mine, ticket);
-                    if (mine) {
-                        put16(RD, 0, slot, pack2d(P.o[0], P.o[1]));
-                        put16(RD, 1, slot, pack2d(P.o[2], P.d[0]));
-                        put16(RD, 2, slot, pack2d(P.d[1], P.d[2]));
-                        put16(RD, 3, slot, pack2d(P.T[0], P.T[1]));
-                        put16(RD, 4, slot, pack2d(P.T[2], acc[0]));
-                        put16(RD, 5, slot, pack2d(acc[1], acc[2]));
-                        put16(RD, 6, slot, Uvec4{lo32(R.tmax), hi32(R.tmax), R.ref, (R.found ? 1u : 0u) | (P.depth << 1)});
-                        put16(RD, 7, slot, Uvec4{P.rng, u_txy, u_cp, s});
-                    }
-                    if (k) ring_publish(RD, mine, ticket, k);
-                    if (mine) R.state = kIdle;
-                }
-            }
-            // ---- empty lanes take FRESH rays --------------------------------------------------
-            {
-                const uint64_t m = __ballot(R.state == kIdle);
-                if (m && ring_count(RF, 1) != 0) {
-                    uint32_t t0;
-                    const uint32_t k = ring_take(RF, 1, 2, static_cast<uint32_t>(__popcll(m)), t0);
-                    const uint32_t r = rank_in(m);
-                    const bool mine = R.state == kIdle && r < k;
-                    const uint32_t ticket = t0 + r, slot = ticket & (kRingCapF - 1);
-                    ring_wait(RF, mine, ticket);
-                    if (mine) {
-                        Uvec4 v = get16(RF, 0, slot);
-                        P.o[0] = dbl(v.x, v.y); P.o[1] = dbl(v.z, v.w);
-                        v = get16(RF, 1, slot);
-                        P.o[2] = dbl(v.x, v.y); P.d[0] = dbl(v.z, v.w);
-                        v = get16(RF, 2, slot);
-                        P.d[1] = dbl(v.x, v.y); P.d[2] = dbl(v.z, v.w);
-                        v = get16(RF, 3, slot);
-                        P.T[0] = dbl(v.x, v.y); P.T[1] = dbl(v.z, v.w);
-                        v = get16(RF, 4, slot);
-                        P.T[2] = dbl(v.x, v.y); acc[0] = dbl(v.z, v.w);
-                        v = get16(RF, 5, slot);
-                        acc[1] = dbl(v.x, v.y); acc[2] = dbl(v.z, v.w);
-                        v = get16(RF, 6, slot);
-                        R.a = dbl(v.x, v.y); R.inv32[0] = __uint_as_float(v.z); R.inv32[1] = __uint_as_float(v.w);
-                        v = get16(RF, 7, slot);
-                        R.inv32[2] = __uint_as_float(v.x); R.oinv32[0] = __uint_as_float(v.y);
-                        R.oinv32[1] = __uint_as_float(v.z); R.oinv32[2] = __uint_as_float(v.w);
-                        v = get16(RF, 8, slot);
-                        R.marg = __uint_as_float(v.x); R.neg = v.y; P.rng = v.z; P.depth = v.w;
-                        v = get16(RF, 9, slot);
-                        u_txy = v.x; u_cp = v.y; s = v.z;
-                        R.tmax = __builtin_inf();
-                        R.tmax32 = 0x1p100f;
-                        R.cur = 0;
-                        R.sp = 0;
-                        R.ref = 0;
-                        R.found = false;
-                        R.state = kWalk;
-                        st.base[-static_cast<ptrdiff_t>(st.stride)] = static_cast<SE>(W.sentinel);
-                    }
-                    if (k) ring_release(RF, mine, ticket, k);
-                }
-            }
-            const int ntrav = __popcll(__ballot(R.state == kWalk || R.state == kLeaf));
-            if (64 - ntrav >= kShadeBatch || ntrav == 0) {
-                shading = true;
-                shade_iters = 0;
-            }
-            if (COUNT) cd += static_cast<uint32_t>(wall_clock64());
-            continue;
-        }
-        // ---- shading: empty lanes take DONE rays, then draw new units ---------------------
-        if (COUNT) cd -= static_cast<uint32_t>(wall_clock64());
-        set_prio<kPrioInit>();
-        {
-            const uint64_t m = __ballot(R.state == kIdle);
-            if (m && ring_count(RD, 1) != 0) {
-                uint32_t t0;
-                const uint32_t k = ring_take(RD, 1, 2, static_cast<uint32_t>(__popcll(m)), t0);
-                const uint32_t r = rank_in(m);
-                const bool mine = R.state == kIdle && r < k;
-                const uint32_t ticket = t0 + r, slot = ticket & (kRingCapD - 1);
-                ring_wait(RD, mine, ticket);
-                if (mine) {
-                    Uvec4 v = get16(RD, 0, slot);
-                    P.o[0] = dbl(v.x, v.y); P.o[1] = dbl(v.z, v.w);
-                    v = get16(RD, 1, slot);
-                    P.o[2] = dbl(v.x, v.y); P.d[0] = dbl(v.z, v.w);
-                    v = get16(RD, 2, slot);
-                    P.d[1] = dbl(v.x, v.y); P.d[2] = dbl(v.z, v.w);
-                    v = get16(RD, 3, slot);
-                    P.T[0] = dbl(v.x, v.y); P.T[1] = dbl(v.z, v.w);
-                    v = get16(RD, 4, slot);
-                    P.T[2] = dbl(v.x, v.y); acc[0] = dbl(v.z, v.w);
-                    v = get16(RD, 5, slot);
-                    acc[1] = dbl(v.x, v.y); acc[2] = dbl(v.z, v.w);
-                    v = get16(RD, 6, slot);
-                    R.tmax = dbl(v.x, v.y); R.ref = v.z; R.found = (v.w & 1u) != 0; P.depth = v.w >> 1;
-                    v = get16(RD, 7, slot);
-                    P.rng = v.x; u_txy = v.y; u_cp = v.z; s = v.w;
-                    R.state = kDone;
-                }
-                if (k) ring_release(RD, mine, ticket, k);
-            }
-        }
-        // lanes still empty draw units (render_kernel's draw loop); start: a new sample to begin
-        bool need = R.state == kIdle, start = false;
-        while (!dry) {
-            const uint64_t m = __ballot(need);
-            if (m == 0) break;
-            if (item_pos >= item_units) {
-                const uint32_t leader = static_cast<uint32_t>(__ffsll(static_cast<long long>(m)) - 1);
-                item_units = 0;
-                item_pos = 0;
-                uint32_t v = 0;
-                if (lane == leader) v = atomicAdd(W.queue, 1u);
-                const uint32_t j = __builtin_amdgcn_readlane(v, leader);
-                const uint32_t nt = W.tiles, bulk = nt * W.groups;
-                if (j < nt * (W.groups + W.tail_chunks)) {
-                    uint32_t tile;
-                    if (j < bulk) {
-                        tile = j / W.groups;
-                        item_chunk = (j - tile * W.groups) * W.item_chunks;
-                        item_units = 64 * W.item_chunks;
-                    } else {
-                        const uint32_t jt = j - bulk;
-                        tile = jt / W.tail_chunks;
-                        item_chunk = W.bulk_chunks + (jt - tile * W.tail_chunks);
-                        item_units = 64;
-                    }
-                    item_txy = (tile % W.tiles_x) | ((tile / W.tiles_x) << 16);
-                } else {
-                    dry = true;
-                    break;
-                }
-            }
-            const uint32_t take = min(static_cast<uint32_t>(__popcll(m)), item_units - item_pos);
-            const uint32_t r = rank_in(m);
-            if (need && r < take) {
-                const uint32_t uu = item_pos + r, pix = uu & 63, chunk = item_chunk + (uu >> 6);
-                u_txy = item_txy;
-                u_cp = (chunk << 6) | pix;
-                const uint32_t col = (item_txy & 0xffffu) * kTileW + pix % kTileW, k = (item_txy >> 16) * kTileH + pix / kTileW;
-                if (chunk < W.chunks && col < W.bw && k < W.bh) {
-                    s = chunk * W.chunk_len;
-                    if (C.max_depth > 0) {
-                        need = false;
-                        start = true;
-                        acc[0] = acc[1] = acc[2] = 0;
-                    } else if (!COUNT) {
-                        double* dst = partial + (static_cast<size_t>(chunk) * W.bh * W.bw + static_cast<size_t>(k) * W.bw + col) * 3;
-                        dst[0] = 0;
-                        dst[1] = 0;
-                        dst[2] = 0;
-                    }
-                }
-            }
-            item_pos += take;
-        }
-        if (COUNT) {
-            const uint32_t now = static_cast<uint32_t>(wall_clock64());
-            cd += now;
-            cs -= now;
-        }
-        // nothing to shade or start: back to tracing, or the end
-        if (__ballot(R.state == kDone || start) == 0) {
-            if (COUNT) cs += static_cast<uint32_t>(wall_clock64());
-            const bool trav = __ballot(R.state == kWalk || R.state == kLeaf) != 0;
-            if (!trav && dry && ring_count(RD, 1) == 0 && ring_count(RF, 1) == 0 &&
-                ring_count(RD, 0) == kRingCapD && ring_count(RF, 0) == kRingCapF)
-                break;  // lanes, queue and rings empty (a record still being read is not ours)
-            shading = false;
-            if (!trav && ring_count(RF, 1) == 0) __builtin_amdgcn_s_sleep(8);
-            continue;
-        }
-        set_prio<kPrioShade>();
-        bool cont = false;
-        if (R.state == kDone) {
-            if (COUNT && wave_leader()) ctr.it_shade++;
-            bool ended = shade<true, kSphOnly, kFlatOnly, kFast>(S, CL, P, R.found, R.ref, R.tmax, acc);
-            if (!ended && P.depth == 0) ended = true;
-            if (!ended) {
-                cont = true;
-            } else {
-                const uint32_t chunk = u_cp >> 6;
-                if (++s < min(C.spp, (chunk + 1) * W.chunk_len)) {
-                    start = true;
-                } else {
-                    if (!COUNT) {
-                        const uint32_t pix = u_cp & 63;
-                        const uint32_t col = (u_txy & 0xffffu) * kTileW + pix % kTileW, k = (u_txy >> 16) * kTileH + pix / kTileW;
-                        double* dst = partial + (static_cast<size_t>(chunk) * W.bh * W.bw + static_cast<size_t>(k) * W.bw + col) * 3;
-                        dst[0] = acc[0];
-                        dst[1] = acc[1];
-                        dst[2] = acc[2];
-                    }
-                }
-                R.state = kIdle;
-            }
-        }
-        if (COUNT) {
-            const uint32_t now = static_cast<uint32_t>(wall_clock64());
-            cs += now;
-            ci -= now;
-        }
-        set_prio<kPrioInit>();
-        if (start) {
-            const uint32_t pix = u_cp & 63;
-            const uint32_t col = W.col0 + (u_txy & 0xffffu) * kTileW + pix % kTileW;
-            const uint32_t row = owned_row(W, W.k0 + (u_txy >> 16) * kTileH + pix / kTileW);
-            start_path(CL, row, col, sample_seed(C.base_seed, row * C.w + col, s), P);
-        }
-        if (start || cont) {
-            st.base[-static_cast<ptrdiff_t>(st.stride)] = static_cast<SE>(W.sentinel);
-            trav_init(P.o, P.d, W.f32_ok != 0, R);
-            if (COUNT) ctr.rays++;
-        }
-        if (COUNT) ci += static_cast<uint32_t>(wall_clock64());
-        if (COUNT && ((ctr.rays | ctr.nodes | ctr.sphere_tests | ctr.quad_tests | ctr.it_walk | ctr.it_leaf |
-                       ctr.it_shade | ctr.slow_nodes | ctr.it_slow | ctr.cand | ctr.it_cand) & 0x80000000u))
-            flush_counts(ctr, counters);
-        // ---- export the fresh rays and shade a batch of DONE rays again, while DONE has them
-        // and FRESH is below its target; else trace them here
-        const bool fresh = start || cont;
-        const uint64_t mf = __ballot(fresh);
-        const uint32_t nfr = ring_count(RF, 1);
-        if (++shade_iters < kMaxShadeIters && mf && nfr < kFreshTarget) {
-            if (COUNT) cd -= static_cast<uint32_t>(wall_clock64());
-            uint32_t t0;
-            const uint32_t want = min(static_cast<uint32_t>(__popcll(mf)), kFreshTarget - nfr);
-            const uint32_t k = ring_take(RF, 0, 3, want, t0);
-            const uint32_t r = rank_in(mf);
-            const bool mine = fresh && r < k;
-            const uint32_t ticket = t0 + r, slot = ticket & (kRingCapF - 1);
-            if (k) ring_slot_free(RF, mine, ticket);
-            if (mine) {
-                put16(RF, 0, slot, pack2d(P.o[0], P.o[1]));
-                put16(RF, 1, slot, pack2d(P.o[2], P.d[0]));
-                put16(RF, 2, slot, pack2d(P.d[1], P.d[2]));
-                put16(RF, 3, slot, pack2d(P.T[0], P.T[1]));
-                put16(RF, 4, slot, pack2d(P.T[2], acc[0]));
-                put16(RF, 5, slot, pack2d(acc[1], acc[2]));
-                put16(RF, 6, slot, Uvec4{lo32(R.a), hi32(R.a), __float_as_uint(R.inv32[0]), __float_as_uint(R.inv32[1])});
-                put16(RF, 7, slot, Uvec4{__float_as_uint(R.inv32[2]), __float_as_uint(R.oinv32[0]), __float_as_uint(R.oinv32[1]),
-                                         __float_as_uint(R.oinv32[2])});
-                put16(RF, 8, slot, Uvec4{__float_as_uint(R.marg), R.neg, P.rng, P.depth});
-                put16(RF, 9, slot, Uvec4{u_txy, u_cp, s, 0u});
-            }
-            if (k) ring_publish(RF, mine, ticket, k);
-            if (mine) R.state = kIdle;
-            if (COUNT) cd += static_cast<uint32_t>(wall_clock64());
-            if (k) continue;  // shading again: the exported lanes take DONE rays
-        }
-        shading = false;
-    }
-    if (COUNT) {
-        using ull = unsigned long long;
-        flush_counts(ctr, counters);
-        if (lane == 0) {
-            atomicAdd(&counters->cyc_walk, static_cast<ull>(cw));
-            atomicAdd(&counters->cyc_leaf, static_cast<ull>(cl));
-            atomicAdd(&counters->cyc_shade, static_cast<ull>(cs));
-            atomicAdd(&counters->cyc_draw, static_cast<ull>(cd));
-            atomicAdd(&counters->cyc_init, static_cast<ull>(ci));
-            atomicAdd(&counters->cyc_total, wall_clock64() - t_start);
-        }
-    }
-}
-
 // pixel_color /= spp (camera.h:290, rgb.h:76): sum the chunks in order, multiply by 1/spp.
 // One thread per pixel of the launch's band.
 __global__ __launch_bounds__(256) void resolve_kernel(const double* __restrict__ partial,
@@ -2399,79 +1923,117 @@ struct DeviceGuard {
 static size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
 // The device image of a scene: every array of device_layout() at its offset in one host buffer,
-// built once per scene (the first upload) and copied whole to each device.
+// built once per scene (the first upload) and copied whole to each device. The derived arrays
+// (f32 nodes, filter records, per-slot material records) are written straight into the image,
+// per element in parallel (parallel_for); the image is not zero-filled first, only the guard words
+// (and the padding, which nothing reads) are cleared.
 static void stage_image(crt_scene* s) {
     const size_t n_nodes = s->dnodes.size(), n_refs = s->refs.size();
     const size_t n_sp = s->spheres.size(), n_q = s->quads.size(), n_m = s->dmats.size();
-    // f32 refs are byte offsets (index << 5) and interior w1 must stay below kLeafFlagF
-    std::vector<DevNodeF> fnodes(n_nodes);
-    bool f32_ok = true;
-    for (size_t i = 0; i < n_nodes; ++i) {
-        const DevNode& n = s->dnodes[i];
-        DevNodeF& f = fnodes[i];
-        for (int k = 0; k < 6; ++k) {
-            f.b[k] = static_cast<float>(n.b[k]);  // round to nearest
-            if (!std::isinf(n.b[k]) && !(std::fabs(n.b[k]) <= kF32BoundMax)) f32_ok = false;
-        }
-        if (n.count == 0 && n.index == n.flags + 1 && !(n.flags & 1u)) {
-            // interior: children side by side, the left one at an even index (stage()); the walk
-            // takes the right child as left | 32
-            f.w0 = n.axis;
-            f.w1 = n.flags << kNodeFShift;
-        } else if (n.count == 0) {
-            // the root of an empty tree (empty box, no children): an empty leaf
-            f.w0 = 0;
-            f.w1 = kLeafFlagF;
-        } else if (n.count == kSentinelCount) {
-            // "axis" 3: R.neg bit 3 (kZeroDir) is clear in the f32 walk, so the far child the
-            // walk stores at the sentinel (into the guard level) is w0 & ~31, the sentinel itself
-            f.w0 = (static_cast<uint32_t>(i) << kNodeFShift) | 3u;
-            f.w1 = kSentinelW1;
-        } else {
-            f.w0 = n.index;
-            f.w1 = kLeafFlagF | n.count;
-        }
+    size_t off[kArrCount + 1];
+    const size_t total = device_layout(s, off);
+    BigVec<char>& img = s->image;
+    img.resize(total);
+    auto at = [&](int arr) { return img.data() + off[arr]; };
+    // padding between the arrays (and the guard words): zero
+    for (int a = 0; a < kArrCount; ++a) {
+        static const size_t kElem[kArrCount] = {sizeof(DevNode), sizeof(DevNodeF), 4, sizeof(DevSphere), sizeof(DevSpherePair),
+                                                4, sizeof(DevQuad), sizeof(DevQuadF), sizeof(DevQuadBox), 4,
+                                                sizeof(DevMaterial), sizeof(DevMaterial), sizeof(DevMaterial), 1};
+        const size_t cnt[kArrCount] = {n_nodes, n_nodes, n_refs, n_sp, n_sp, n_sp, n_q, n_q, n_q, n_q, n_m, n_sp, n_q, 64};
+        const size_t used = a == kArrGuard ? 0 : cnt[a] * kElem[a];
+        std::memset(img.data() + off[a] + used, 0, off[a + 1] - off[a] - used);
     }
-    // sphere pair records of the f32 candidate filter (slots i, i + 1)
-    std::vector<DevSpherePair> spair(n_sp);
-    bool spheres_f32_ok = true;
-    for (size_t i = 0; i < n_sp; ++i) {
+    // plain copies, in parallel chunks
+    auto put = [&](int arr, const void* src, size_t bytes) {
+        char* dst = at(arr);
+        const char* sp = static_cast<const char*>(src);
+        parallel_for(bytes, size_t{1} << 22, [&](size_t a, size_t b) { std::memcpy(dst + a, sp + a, b - a); });
+    };
+    put(kArrNodes, s->dnodes.data(), n_nodes * sizeof(DevNode));
+    put(kArrRefs, s->refs.data(), n_refs * 4);
+    put(kArrSpheres, s->spheres.data(), n_sp * sizeof(DevSphere));
+    put(kArrSphereMat, s->sphere_mat.data(), n_sp * 4);
+    put(kArrQuads, s->quads.data(), n_q * sizeof(DevQuad));
+    put(kArrQuadMat, s->quad_mat.data(), n_q * 4);
+    put(kArrMats, s->dmats.data(), n_m * sizeof(DevMaterial));
+    // f32 refs are byte offsets (index << 5) and interior w1 must stay below kLeafFlagF
+    DevNodeF* fnodes = reinterpret_cast<DevNodeF*>(at(kArrFNodes));
+    std::atomic<bool> f32_bad{false};
+    parallel_for(n_nodes, 4096, [&](size_t a, size_t b) {
+        bool bad = false;
+        for (size_t i = a; i < b; ++i) {
+            const DevNode& n = s->dnodes[i];
+            DevNodeF& f = fnodes[i];
+            for (int k = 0; k < 6; ++k) {
+                f.b[k] = static_cast<float>(n.b[k]);  // round to nearest
+                if (!std::isinf(n.b[k]) && !(std::fabs(n.b[k]) <= kF32BoundMax)) bad = true;
+            }
+            if (n.count == 0 && n.index == n.flags + 1 && !(n.flags & 1u)) {
+                // interior: children side by side, the left one at an even index (stage()); the walk
+                // takes the right child as left | 32
+                f.w0 = n.axis;
+                f.w1 = n.flags << kNodeFShift;
+            } else if (n.count == 0) {
+                // the root of an empty tree (empty box, no children): an empty leaf
+                f.w0 = 0;
+                f.w1 = kLeafFlagF;
+            } else if (n.count == kSentinelCount) {
+                // "axis" 3: R.neg bit 3 (kZeroDir) is clear in the f32 walk, so the far child the
+                // walk stores at the sentinel (into the guard level) is w0 & ~31, the sentinel itself
+                f.w0 = (static_cast<uint32_t>(i) << kNodeFShift) | 3u;
+                f.w1 = kSentinelW1;
+            } else {
+                f.w0 = n.index;
+                f.w1 = kLeafFlagF | n.count;
+            }
+        }
+        if (bad) f32_bad = true;
+    });
+    // sphere pair records of the f32 candidate filter (slots i, i + 1): half i of record i from
+    // sphere i, the other half from sphere i + 1 (the last record's second half zero)
+    DevSpherePair* spair = reinterpret_cast<DevSpherePair*>(at(kArrSpherePairs));
+    std::atomic<bool> sph_bad{false};
+    auto pair_half = [&](size_t i, float& cx, float& cy, float& cz, float& r2e) {
         const DevSphere& sp = s->spheres[i];
         double dc2 = 0;
+        bool bad = false;
         for (int k = 0; k < 3; ++k) {
-            if (!(std::fabs(sp.c[k]) <= kF32SphereMax)) spheres_f32_ok = false;
+            if (!(std::fabs(sp.c[k]) <= kF32SphereMax)) bad = true;
             const double e = sp.c[k] - static_cast<double>(static_cast<float>(sp.c[k]));
             dc2 += e * e;
         }
-        if (!(std::fabs(sp.r) <= kF32SphereMax)) spheres_f32_ok = false;
-        const float cx = static_cast<float>(sp.c[0]), cy = static_cast<float>(sp.c[1]), cz = static_cast<float>(sp.c[2]);
-        const float r2e = static_cast<float>(sp.r * sp.r * (1 + 0x1p-14) + dc2 * 0x1p22);
-        spair[i].cx[0] = cx; spair[i].cy[0] = cy; spair[i].cz[0] = cz; spair[i].r2e[0] = r2e;
-        if (i > 0) {
-            spair[i - 1].cx[1] = cx; spair[i - 1].cy[1] = cy; spair[i - 1].cz[1] = cz; spair[i - 1].r2e[1] = r2e;
+        if (!(std::fabs(sp.r) <= kF32SphereMax)) bad = true;
+        cx = static_cast<float>(sp.c[0]);
+        cy = static_cast<float>(sp.c[1]);
+        cz = static_cast<float>(sp.c[2]);
+        r2e = static_cast<float>(sp.r * sp.r * (1 + 0x1p-14) + dc2 * 0x1p22);
+        return bad;
+    };
+    parallel_for(n_sp, 4096, [&](size_t a, size_t b) {
+        bool bad = false;
+        for (size_t i = a; i < b; ++i) {
+            DevSpherePair& r = spair[i];
+            bad = pair_half(i, r.cx[0], r.cy[0], r.cz[0], r.r2e[0]) || bad;
+            if (i + 1 < n_sp) (void)pair_half(i + 1, r.cx[1], r.cy[1], r.cz[1], r.r2e[1]);
+            else r.cx[1] = r.cy[1] = r.cz[1] = r.r2e[1] = 0;
         }
-    }
-    if (n_sp) {
-        DevSpherePair& last = spair[n_sp - 1];
-        last.cx[1] = last.cy[1] = last.cz[1] = last.r2e[1] = 0;
-    }
-    // parallelogram filter records (crt_quad_filter.h quad_record)
-    std::vector<DevQuadF> quadf(n_q);
-    std::vector<DevQuadBox> quadbox(n_q);
-    bool quads_f32_ok = true, quads_flat_ok = true;
-    for (size_t i = 0; i < n_q; ++i) {
-        const DevQuad& q = s->quads[i];
-        if (!quad_record(q.v, q.s1, q.s2, q.sn, quadf[i])) quads_f32_ok = false;
-        if (!quad_flat_box(q.v, q.s1, q.s2, quadbox[i])) quads_flat_ok = false;
-    }
-    size_t off[kArrCount + 1];
-    const size_t total = device_layout(s, off);
-    const size_t off_nodes = off[kArrNodes], off_fnodes = off[kArrFNodes], off_refs = off[kArrRefs];
-    const size_t off_sp = off[kArrSpheres], off_spp = off[kArrSpherePairs], off_spm = off[kArrSphereMat];
-    const size_t off_q = off[kArrQuads], off_qf = off[kArrQuadF], off_qb = off[kArrQuadBox];
-    const size_t off_qm = off[kArrQuadMat], off_m = off[kArrMats], off_smr = off[kArrSphereMrec];
-    const size_t off_qmr = off[kArrQuadMrec], off_guard = off[kArrGuard];
-    std::vector<DevMaterial> smrec(n_sp), qmrec(n_q);
+        if (bad) sph_bad = true;
+    });
+    // parallelogram filter records (crt_quad_filter.h quad_record, quad_flat_box)
+    DevQuadF* quadf = reinterpret_cast<DevQuadF*>(at(kArrQuadF));
+    DevQuadBox* quadbox = reinterpret_cast<DevQuadBox*>(at(kArrQuadBox));
+    std::atomic<bool> quads_bad{false}, flat_bad{false};
+    parallel_for(n_q, 4096, [&](size_t a, size_t b) {
+        bool qb = false, fb = false;
+        for (size_t i = a; i < b; ++i) {
+            const DevQuad& q = s->quads[i];
+            if (!quad_record(q.v, q.s1, q.s2, q.sn, quadf[i])) qb = true;
+            if (!quad_flat_box(q.v, q.s1, q.s2, quadbox[i])) fb = true;
+        }
+        if (qb) quads_bad = true;
+        if (fb) flat_bad = true;
+    });
     // Shading constants precomputed per slot, with the reference's own operations (IEEE f64, no
     // contraction), so shade reads the values its divisions would give:
     //   emit[0] of a non-emitting sphere slot = 1 / r (the normal's (p - c) / r, vec3d.h:34);
@@ -2489,37 +2051,24 @@ static void stage_image(crt_scene* s) {
         }
         if (sp && m.kind != CRT_DIFFUSE_LIGHT) m.emit[0] = 1 / sp->r;
     };
-    for (size_t i = 0; i < n_sp; ++i) {
-        smrec[i] = s->dmats[s->sphere_mat[i]];
-        shading_consts(smrec[i], &s->spheres[i]);
-    }
-    for (size_t i = 0; i < n_q; ++i) {
-        qmrec[i] = s->dmats[s->quad_mat[i]];
-        shading_consts(qmrec[i], nullptr);
-    }
-    std::vector<char>& img = s->image;
-    img.assign(total, 0);  // the guard words upload as zeros
-    auto put = [&](size_t off, const void* src, size_t bytes) {
-        if (bytes) std::memcpy(img.data() + off, src, bytes);
-    };
-    put(off_nodes, s->dnodes.data(), n_nodes * sizeof(DevNode));
-    put(off_fnodes, fnodes.data(), n_nodes * sizeof(DevNodeF));
-    put(off_refs, s->refs.data(), n_refs * 4);
-    put(off_sp, s->spheres.data(), n_sp * sizeof(DevSphere));
-    put(off_spp, spair.data(), n_sp * sizeof(DevSpherePair));
-    put(off_spm, s->sphere_mat.data(), n_sp * 4);
-    put(off_q, s->quads.data(), n_q * sizeof(DevQuad));
-    put(off_qf, quadf.data(), n_q * sizeof(DevQuadF));
-    put(off_qb, quadbox.data(), n_q * sizeof(DevQuadBox));
-    put(off_qm, s->quad_mat.data(), n_q * 4);
-    put(off_m, s->dmats.data(), n_m * sizeof(DevMaterial));
-    put(off_smr, smrec.data(), n_sp * sizeof(DevMaterial));
-    put(off_qmr, qmrec.data(), n_q * sizeof(DevMaterial));
-    (void)off_guard;
-    s->image_f32_ok = f32_ok;
-    s->image_spheres_f32_ok = spheres_f32_ok;
-    s->image_quads_f32_ok = quads_f32_ok;
-    s->image_quads_flat_ok = quads_flat_ok;
+    DevMaterial* smrec = reinterpret_cast<DevMaterial*>(at(kArrSphereMrec));
+    DevMaterial* qmrec = reinterpret_cast<DevMaterial*>(at(kArrQuadMrec));
+    parallel_for(n_sp, 4096, [&](size_t a, size_t b) {
+        for (size_t i = a; i < b; ++i) {
+            smrec[i] = s->dmats[s->sphere_mat[i]];
+            shading_consts(smrec[i], &s->spheres[i]);
+        }
+    });
+    parallel_for(n_q, 4096, [&](size_t a, size_t b) {
+        for (size_t i = a; i < b; ++i) {
+            qmrec[i] = s->dmats[s->quad_mat[i]];
+            shading_consts(qmrec[i], nullptr);
+        }
+    });
+    s->image_f32_ok = !f32_bad;
+    s->image_spheres_f32_ok = !sph_bad;
+    s->image_quads_f32_ok = !quads_bad;
+    s->image_quads_flat_ok = !flat_bad;
     s->staged = true;
 }
 
@@ -2648,11 +2197,7 @@ static size_t partial_budget() {
     return size_t{4} << 30;
 }
 
-// render_pool_kernel's rings (DONE then FRESH: control words, flags, records)
-constexpr size_t kPoolRingBytes = (16 + dev::kRingCapD * 4 + dev::kDoneChunks * dev::kRingCapD * 16) +
-                                  (16 + dev::kRingCapF * 4 + dev::kFreshChunks * dev::kRingCapF * 16);
-
-template <typename SE, bool GSTACK, bool LSCENE, int PM, bool W5 = false, bool POOL = false>
+template <typename SE, bool GSTACK, bool LSCENE, int PM, bool W5 = false>
 static int launch_render(const crt_scene* s, int device, const crt_camera* cam, const dev::Work& w0,
                          size_t lds, double* d_rgb, hipStream_t stream, crt_render_stats* count_stats) {
     const DeviceCopy& c = s->dev[device];
@@ -2663,14 +2208,8 @@ static int launch_render(const crt_scene* s, int device, const crt_camera* cam, 
         W.lds_acc = static_cast<uint32_t>(align16(lds));
         lds = W.lds_acc + kAccBytes;
     }
-    if (POOL) {  // then the ray-exchange rings
-        W.lds_pool = static_cast<uint32_t>(align16(lds));
-        lds = W.lds_pool + kPoolRingBytes;
-    }
-    constexpr int kThreads = POOL ? dev::kPoolBlock : dev::kBlock;
-    const void* kfn = nullptr;
-    if constexpr (POOL) kfn = reinterpret_cast<const void*>(dev::render_pool_kernel<SE, PM, false>);
-    else kfn = reinterpret_cast<const void*>(dev::render_kernel<SE, GSTACK, LSCENE, false, PM, W5>);
+    constexpr int kThreads = dev::kBlock;
+    const void* kfn = reinterpret_cast<const void*>(dev::render_kernel<SE, GSTACK, LSCENE, false, PM, W5>);
     const uint64_t pixels = static_cast<uint64_t>(W.owned_rows) * cam->image_w;
     // Sample chunks: a function of spp ONLY, so every pixel's sum is grouped identically whatever
     // the tiling / number of GPUs / lane schedule / band split (bit-identical frames for 1..N
@@ -2702,7 +2241,6 @@ static int launch_render(const crt_scene* s, int device, const crt_camera* cam, 
     int cus = 0, per_cu = 0;
     HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
     HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, kThreads, lds));
-    if (POOL && per_cu < 1) return fail(CRT_E_INVALID, "render_pool_kernel does not fit a CU");
     constexpr uint32_t kWavesPerBlock = kThreads / 64;
     uint64_t resident = static_cast<uint64_t>(std::max(1, cus)) * std::max(1, per_cu);
     if (const char* e = std::getenv("CRT_GRID_BLOCKS"))  // schedule tests: a smaller grid, same frame
@@ -2779,23 +2317,15 @@ static int launch_render(const crt_scene* s, int device, const crt_camera* cam, 
             // HBM-resident scenes: one queue per XCD (blocks b and b + 8 share one), so an XCD's L2
             // serves the rays of one region of the band (config 4: 163.5 vs 166.2 ms); LDS scenes
             // keep one queue (config 2: 88.5 vs 89.0 ms with eight). CRT_XCD_QUEUES=0/1 forces.
-            W.segments = !POOL && knob("CRT_XCD_QUEUES", LSCENE ? 0 : 1) ? 8u : 1u;
+            W.segments = knob("CRT_XCD_QUEUES", LSCENE ? 0 : 1) ? 8u : 1u;
             HIP_TRY(hipMemsetAsync(queue, 0, 8 * sizeof(uint32_t), stream));
             if (count) {
-                if constexpr (POOL)
-                    hipLaunchKernelGGL((dev::render_pool_kernel<SE, PM, true>), dim3(static_cast<uint32_t>(blocks)),
-                                       dim3(kThreads), lds, stream, S, C, W, partial, ctr);
-                else
-                    hipLaunchKernelGGL((dev::render_kernel<SE, GSTACK, LSCENE, true, PM, W5>), dim3(static_cast<uint32_t>(blocks)),
-                                       dim3(dev::kBlock), lds, stream, S, C, W, partial, gstack, ctr);
+                hipLaunchKernelGGL((dev::render_kernel<SE, GSTACK, LSCENE, true, PM, W5>), dim3(static_cast<uint32_t>(blocks)),
+                                   dim3(dev::kBlock), lds, stream, S, C, W, partial, gstack, ctr);
                 HIP_TRY(hipGetLastError());
             } else {
-                if constexpr (POOL)
-                    hipLaunchKernelGGL((dev::render_pool_kernel<SE, PM, false>), dim3(static_cast<uint32_t>(blocks)),
-                                       dim3(kThreads), lds, stream, S, C, W, partial, ctr);
-                else
-                    hipLaunchKernelGGL((dev::render_kernel<SE, GSTACK, LSCENE, false, PM, W5>), dim3(static_cast<uint32_t>(blocks)),
-                                       dim3(dev::kBlock), lds, stream, S, C, W, partial, gstack, ctr);
+                hipLaunchKernelGGL((dev::render_kernel<SE, GSTACK, LSCENE, false, PM, W5>), dim3(static_cast<uint32_t>(blocks)),
+                                   dim3(dev::kBlock), lds, stream, S, C, W, partial, gstack, ctr);
                 HIP_TRY(hipGetLastError());
                 const uint64_t rb = (static_cast<uint64_t>(W.bw) * W.bh + 255) / 256;
                 hipLaunchKernelGGL(dev::resolve_kernel, dim3(static_cast<uint32_t>(rb)), dim3(256), 0, stream, partial,
@@ -2884,24 +2414,6 @@ static int dispatch_render(const crt_scene* s, int device, const crt_camera* cam
         W.lds_quadf = W.lds_quads + W.bytes_quads;
         W.lds_sph64 = W.lds_quadf + W.bytes_quadf;
         const size_t cam_bytes = align16(sizeof(dev::CamView));
-        // CRT_POOL=1: the block-level ray exchange (render_pool_kernel, one 1024-thread block a CU
-        // with the scene, its stacks and the rings in 160 KB of LDS) for sphere-only and flat
-        // parallelogram scenes
-        if (std::getenv("CRT_POOL") != nullptr && (W.sphere_only || W.quads_flat)) {
-            const uint32_t plevel = static_cast<uint32_t>(dev::kPoolBlock * sizeof(SE));
-            const size_t pstack = align16(static_cast<size_t>(s->depth + 1) * plevel);
-            auto pstack_at = [&](size_t data) { return std::max<size_t>(data, plevel) + plevel; };
-            constexpr size_t kCuLds = 160 * 1024;
-            const uint32_t sph64 = static_cast<uint32_t>(s->spheres.size() * sizeof(DevSphere));
-            const size_t fixed = pstack + cam_bytes + 16 + kPoolRingBytes;
-            if (pstack_at(scene_bytes) + fixed <= kCuLds) {
-                W.bytes_sph64 = (W.spheres_f32 && pstack_at(scene_bytes + sph64) + fixed <= kCuLds) ? sph64 : 0u;
-                W.lds_stack = static_cast<uint32_t>(pstack_at(scene_bytes + W.bytes_sph64));
-                const size_t plds = W.lds_stack + pstack;
-                if (W.sphere_only) return launch_render<SE, false, true, 0, false, true>(s, device, cam, W, plds, d_rgb, st, count_stats);
-                return launch_render<SE, false, true, 2, false, true>(s, device, cam, W, plds, d_rgb, st, count_stats);
-            }
-        }
         // Sphere-only scenes and scenes of axis-aligned parallelograms run five waves per SIMD when
         // five blocks fit a CU's LDS (32 KB each), staging the f64 spheres only if they fit that
         // too (config 2: 73.7 ms at five waves without them vs 75.8 at four with them; config 3:
@@ -2927,7 +2439,7 @@ static int dispatch_render(const crt_scene* s, int device, const crt_camera* cam
     // HBM scene: the top of the (breadth-first) node array goes to LDS as far as it fits beside
     // the stack without costing resident blocks (CRT_WAVES_PER_EU blocks of 4 waves, the VGPR
     // limit); W.ntop counts bytes of f32 nodes
-    const size_t per_block = 160 * 1024 / CRT_WAVES_PER_EU;  // LDS per block at the VGPR occupancy
+    const size_t per_block = 160 * 1024 * dev::kBlock / (256 * CRT_WAVES_PER_EU);  // LDS per block at the VGPR occupancy
     const bool no_top = std::getenv("CRT_NO_LDS_TOP") != nullptr;
     const size_t all_nodes = s->dnodes.size() * sizeof(DevNodeF);
     auto top_bytes = [&](size_t room) {

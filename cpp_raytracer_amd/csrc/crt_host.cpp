@@ -6,6 +6,7 @@
 // to the ones the reference computes. Citations are paths in DeltaPavonis/cpp_raytracer.
 #include <algorithm>
 #include <atomic>
+#include <sys/mman.h>
 #include <chrono>
 #include <cmath>
 #include <cstdint>
@@ -28,6 +29,22 @@ namespace crt {
 
 // ---------------------------------------------------------------------------------------------
 // errors
+void* big_alloc(size_t bytes) {
+    constexpr size_t kHuge = size_t{2} << 20, kMin = size_t{32} << 20;
+    static const bool off = std::getenv("CRT_NO_HUGEPAGES") != nullptr;
+    if (bytes < kMin || off) {
+        void* p = std::malloc(std::max<size_t>(bytes, 1));
+        if (!p) throw std::bad_alloc();
+        return p;
+    }
+    const size_t rounded = (bytes + kHuge - 1) / kHuge * kHuge;
+    void* p = std::aligned_alloc(kHuge, rounded);
+    if (!p) throw std::bad_alloc();
+    (void)madvise(p, rounded, MADV_HUGEPAGE);
+    return p;
+}
+void big_free(void* p, size_t) noexcept { std::free(p); }
+
 static thread_local std::string g_last_error;
 
 int fail(int code, const std::string& msg) {
@@ -70,25 +87,6 @@ static inline double gfmax(double x, double y) {
     if (std::isnan(x)) return y;
     if (std::isnan(y)) return x;
     return x > y ? x : y;
-}
-
-// f(begin, end) over [0, n) in contiguous chunks on up to 16 threads (scene preparation of
-// multi-million-primitive scenes; every element is written by exactly one thread).
-template <typename F>
-static void parallel_for(size_t n, size_t min_chunk, F&& f) {
-    const size_t hw = std::max(1u, std::thread::hardware_concurrency());
-    const size_t nt = std::min<size_t>(std::min<size_t>(hw, 16), (n + min_chunk - 1) / min_chunk);
-    if (nt <= 1) {
-        f(size_t(0), n);
-        return;
-    }
-    const size_t per = (n + nt - 1) / nt;
-    std::vector<std::thread> th;
-    for (size_t t = 0; t < nt; ++t) {
-        const size_t a = t * per, b = std::min(n, a + per);
-        if (a < b) th.emplace_back([&f, a, b] { f(a, b); });
-    }
-    for (auto& x : th) x.join();
 }
 
 // ---- intervals / AABB (math/interval.h, acceleration/aabb.h) --------------------------------
@@ -213,6 +211,7 @@ static int flatten(crt_scene* s, bool boxes) {
         if (k < CRT_LAMBERTIAN || k > CRT_DIFFUSE_LIGHT)
             return fail(CRT_E_INVALID, "material " + std::to_string(i) + " has unknown kind");
     }
+    const auto tv = std::chrono::steady_clock::now();
     s->prims.resize(off[no]);
     // boxes: the GPU BVH build's input, written while the primitives are hot in cache
     if (boxes) s->pbox.resize(off[no] * 6);
@@ -232,7 +231,9 @@ static int flatten(crt_scene* s, bool boxes) {
     });
     // the GPU build reproduces the host fold only for NaN-free boxes (with a NaN, fmin/fmax pick
     // by operand order in ways its order-preserving keys do not model): such scenes build on the host
-    if (nan_box) std::vector<double>().swap(s->pbox);
+    if (nan_box) BigVec<double>().swap(s->pbox);
+    if (std::getenv("CRT_DEBUG_BUILD"))
+        std::fprintf(stderr, "flatten: emit %.3f ms\n", std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tv).count());
     return CRT_OK;
 }
 
@@ -248,14 +249,14 @@ struct TreeNode {
 };
 
 struct Builder {
-    const std::vector<Prim>& prims;
-    std::vector<uint32_t>& order;
+    const BigVec<Prim>& prims;
+    BigVec<uint32_t>& order;
     size_t nb, max_leaf;
     size_t total = 0;
     std::vector<Box3> boxes;
     std::vector<V3> cents;
 
-    Builder(const std::vector<Prim>& p, std::vector<uint32_t>& o, size_t nb_, size_t ml)
+    Builder(const BigVec<Prim>& p, BigVec<uint32_t>& o, size_t nb_, size_t ml)
         : prims(p), order(o), nb(nb_), max_leaf(ml) {
         boxes.resize(p.size());
         cents.resize(p.size());
@@ -348,7 +349,7 @@ struct Builder {
     }
 };
 
-void flatten_tree(const TreeNode* t, std::vector<crt_bvh_node>& out, size_t& next, uint32_t lvl,
+void flatten_tree(const TreeNode* t, BigVec<crt_bvh_node>& out, size_t& next, uint32_t lvl,
                   uint32_t& depth, uint32_t& max_leaf) {
     size_t me = next++;
     depth = std::max(depth, lvl);
@@ -401,7 +402,7 @@ static int build_bvh(crt_scene* s, const crt_bvh_params& prm) {
         // centroids are computed there (Builder's box_of(...).centroid())
         int rc = device_build_bvh(s, prm.num_buckets, prm.max_prims_in_node,
                                   static_cast<int>(prm.build_device) - 1, s->pbox);
-        std::vector<double>().swap(s->pbox);
+        BigVec<double>().swap(s->pbox);
         if (rc) return rc;
     } else {
         if (prm.num_buckets < 2) return fail(CRT_E_INVALID, "num_buckets must be >= 2");
@@ -411,7 +412,7 @@ static int build_bvh(crt_scene* s, const crt_bvh_params& prm) {
         size_t next = 0;
         flatten_tree(root.get(), s->nodes, next, 1, s->depth, s->max_leaf);
     }
-    std::vector<double>().swap(s->pbox);
+    BigVec<double>().swap(s->pbox);
     s->build_ms =
         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return CRT_OK;
@@ -442,6 +443,14 @@ static void stage(crt_scene* s) {
     // that live in HBM).
     constexpr size_t kTopBfs = 1024;
     const size_t nn = s->nodes.size();
+    const bool dbg = std::getenv("CRT_DEBUG_BUILD") != nullptr;
+    auto t0 = std::chrono::steady_clock::now();
+    auto lap = [&](const char* what) {
+        if (!dbg) return;
+        const auto now = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "stage: %-8s %8.3f ms\n", what, std::chrono::duration<double, std::milli>(now - t0).count());
+        t0 = now;
+    };
     auto interior = [&](uint32_t i) {
         return s->nodes[i].count == 0 && !(s->nodes[i].flags & kNodeAlways) && i + 1 < nn;
     };
@@ -517,6 +526,7 @@ static void stage(crt_scene* s) {
         d.axis = n.axis;
         d.flags = inner ? pos[bfs[q] + 1] : n.flags;
     }
+    lap("nodes");
     // slot arrays: per chunk of slots count the spheres, then fill at prefix offsets (the sphere /
     // parallelogram arrays are in slot order either way)
     const size_t ns = s->order.size();
@@ -565,19 +575,23 @@ static void stage(crt_scene* s) {
             }
         }
     });
+    lap("slots");
     s->dmats.resize(s->materials.size());
-    for (size_t i = 0; i < s->materials.size(); ++i) {
-        const crt_material& m = s->materials[i];
-        DevMaterial& d = s->dmats[i];
-        d = DevMaterial{};
-        d.kind = m.kind;
-        d.color[0] = m.color[0]; d.color[1] = m.color[1]; d.color[2] = m.color[2];
-        d.param = m.param;
-        if (m.kind == CRT_DIFFUSE_LIGHT) {
-            // DiffuseLight::emit(): intensity * intrinsic_color -> each channel * intensity
-            for (int k = 0; k < 3; ++k) d.emit[k] = m.color[k] * m.param;
+    parallel_for(s->materials.size(), 1 << 14, [&](size_t a, size_t b) {
+        for (size_t i = a; i < b; ++i) {
+            const crt_material& m = s->materials[i];
+            DevMaterial& d = s->dmats[i];
+            d = DevMaterial{};
+            d.kind = m.kind;
+            d.color[0] = m.color[0]; d.color[1] = m.color[1]; d.color[2] = m.color[2];
+            d.param = m.param;
+            if (m.kind == CRT_DIFFUSE_LIGHT) {
+                // DiffuseLight::emit(): intensity * intrinsic_color -> each channel * intensity
+                for (int k = 0; k < 3; ++k) d.emit[k] = m.color[k] * m.param;
+            }
         }
-    }
+    });
+    lap("materials");
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1076,15 +1090,34 @@ int crt_scene_create(const crt_material* materials, size_t num_materials,
     std::unique_ptr<crt_scene> s;
     try {
         s = std::make_unique<crt_scene>();
-        s->materials.assign(materials, materials + num_materials);
-        s->objects.assign(objects, objects + num_objects);
+        const bool dbg = std::getenv("CRT_DEBUG_BUILD") != nullptr;
+        auto t0 = std::chrono::steady_clock::now();
+        auto lap = [&](const char* what) {  // CRT_DEBUG_BUILD: scene creation phases
+            if (!dbg) return;
+            const auto now = std::chrono::steady_clock::now();
+            std::fprintf(stderr, "scene phase %-8s %8.3f ms\n", what, std::chrono::duration<double, std::milli>(now - t0).count());
+            t0 = now;
+        };
+        // copied in parallel chunks into huge-page backed arrays (millions: 2.1 M objects and materials)
+        s->materials.resize(num_materials);
+        s->objects.resize(num_objects);
+        parallel_for(num_materials, 1 << 15, [&](size_t a, size_t b) {
+            std::memcpy(s->materials.data() + a, materials + a, (b - a) * sizeof(crt_material));
+        });
+        parallel_for(num_objects, 1 << 15, [&](size_t a, size_t b) {
+            std::memcpy(s->objects.data() + a, objects + a, (b - a) * sizeof(crt_object));
+        });
+        lap("copy");
         int rc = flatten(s.get(), prm.build_device != 0 && prm.linear == 0);
         if (rc) return rc;
+        lap("flatten");
         if (s->prims.size() >= 0x7fffffffu) return fail(CRT_E_INVALID, "too many primitives");
         s->linear = prm.linear != 0;
         rc = build_bvh(s.get(), prm);
         if (rc) return rc;
+        lap("build");
         stage(s.get());
+        lap("stage");
     } catch (const std::bad_alloc&) {
         return fail(CRT_E_ALLOC, "out of host memory building the scene");
     }

@@ -3,9 +3,14 @@
 #pragma once
 
 #include <cstddef>
+#include <algorithm>
 #include <cstdint>
+#include <memory>
 #include <mutex>
+#include <type_traits>
+#include <utility>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/crt_render.h"
@@ -14,6 +19,57 @@
 namespace crt {
 
 constexpr int kMaxDevices = 16;
+
+// Allocator whose resize() leaves trivially constructible elements uninitialized: the host staging
+// arrays of multi-million-primitive scenes are written in full right after they are sized, and
+// zero-filling them first cost a serial pass over hundreds of MB.
+// Blocks of 32 MB and more are 2 MB aligned and advised as transparent huge pages: first-touch
+// page faults of 4 KB pages (90k for the millions scene's primitive array alone) dominated its
+// preparation.
+void* big_alloc(size_t bytes);
+void big_free(void* p, size_t bytes) noexcept;
+template <typename T>
+struct NoInitAlloc : std::allocator<T> {
+    using value_type = T;
+    template <typename U>
+    struct rebind {
+        using other = NoInitAlloc<U>;
+    };
+    NoInitAlloc() = default;
+    template <typename U>
+    NoInitAlloc(const NoInitAlloc<U>&) noexcept {}
+    T* allocate(size_t n) { return static_cast<T*>(big_alloc(n * sizeof(T))); }
+    void deallocate(T* p, size_t n) noexcept { big_free(p, n * sizeof(T)); }
+    template <typename U>
+    void construct(U* p) noexcept(std::is_nothrow_default_constructible_v<U>) {
+        ::new (static_cast<void*>(p)) U;
+    }
+    template <typename U, typename... Args>
+    void construct(U* p, Args&&... args) {
+        ::new (static_cast<void*>(p)) U(std::forward<Args>(args)...);
+    }
+};
+template <typename T>
+using BigVec = std::vector<T, NoInitAlloc<T>>;
+
+// f(begin, end) over [0, n) in contiguous chunks on up to 16 threads (scene preparation of
+// multi-million-primitive scenes; every element is written by exactly one thread).
+template <typename F>
+inline void parallel_for(size_t n, size_t min_chunk, F&& f) {
+    const size_t hw = std::max(1u, std::thread::hardware_concurrency());
+    const size_t nt = std::min<size_t>(std::min<size_t>(hw, 16), (n + min_chunk - 1) / min_chunk);
+    if (nt <= 1) {
+        f(size_t(0), n);
+        return;
+    }
+    const size_t per = (n + nt - 1) / nt;
+    std::vector<std::thread> th;
+    for (size_t t = 0; t < nt; ++t) {
+        const size_t a = t * per, b = std::min(n, a + per);
+        if (a < b) th.emplace_back([&f, a, b] { f(a, b); });
+    }
+    for (auto& x : th) x.join();
+}
 
 // ---- HBM layout (one copy per device) ------------------------------------------------------
 // BVH node: the LinearBVHNode of bvh.h:117-161 packed into one 64-byte line (4 x dwordx4 loads).
@@ -134,20 +190,20 @@ struct Prim {
 }  // namespace crt
 
 struct crt_scene {
-    std::vector<crt_material> materials;
-    std::vector<crt_object> objects;
-    std::vector<crt::Prim> prims;
-    std::vector<double> pbox;              // primitive boxes, 6 doubles each (GPU BVH build only)
-    std::vector<crt_bvh_node> nodes;
-    std::vector<uint32_t> order;           // slot -> primitive index
+    crt::BigVec<crt_material> materials;
+    crt::BigVec<crt_object> objects;
+    crt::BigVec<crt::Prim> prims;
+    crt::BigVec<double> pbox;              // primitive boxes, 6 doubles each (GPU BVH build only)
+    crt::BigVec<crt_bvh_node> nodes;
+    crt::BigVec<uint32_t> order;           // slot -> primitive index
     // device-layout staging (host)
-    std::vector<crt::DevNode> dnodes;
-    std::vector<uint32_t> refs;
-    std::vector<crt::DevSphere> spheres;
-    std::vector<uint32_t> sphere_mat;
-    std::vector<crt::DevQuad> quads;
-    std::vector<uint32_t> quad_mat;
-    std::vector<crt::DevMaterial> dmats;
+    crt::BigVec<crt::DevNode> dnodes;
+    crt::BigVec<uint32_t> refs;
+    crt::BigVec<crt::DevSphere> spheres;
+    crt::BigVec<uint32_t> sphere_mat;
+    crt::BigVec<crt::DevQuad> quads;
+    crt::BigVec<uint32_t> quad_mat;
+    crt::BigVec<crt::DevMaterial> dmats;
     uint32_t depth = 0;
     uint32_t max_leaf = 0;
     double build_ms = 0;
@@ -156,7 +212,7 @@ struct crt_scene {
     crt::DeviceCopy dev[crt::kMaxDevices];
     std::mutex dev_mu[crt::kMaxDevices];  // one upload per device at a time (device_upload)
     // the device image (device_layout arrays at their offsets), staged by the first upload
-    std::vector<char> image;
+    crt::BigVec<char> image;
     bool staged = false;
     bool image_f32_ok = false, image_spheres_f32_ok = false, image_quads_f32_ok = false, image_quads_flat_ok = false;
     std::mutex mu;  // staging
@@ -199,7 +255,7 @@ int device_count(int* n);
 const char* device_build_info();
 int device_guard(crt_scene* s, int device, uint64_t* schlick_undecided, bool reset);
 int device_build_bvh(crt_scene* s, uint32_t num_buckets, uint32_t max_leaf, int device,
-                     const std::vector<double>& boxes);
+                     const BigVec<double>& boxes);
 int device_ppm_values(int device, const double* d_rgb, size_t n, int32_t* h_values, void* stream);
 // host: RGB::as_string's three integers for one pixel (std::pow, x86 int conversion)
 void ppm_pixel_host(const double rgb[3], int32_t out[3]);
