@@ -345,8 +345,16 @@ def main() -> int:
     samples_total = h * w * args.spp * args.steps
     ms_per_step = elapsed * 1e3 / max(1, args.steps)
 
-    # algorithmic bytes of one launch (this rank's tile), from the instrumented pass (untimed)
+    # algorithmic bytes of one launch (this rank's tile), from the instrumented pass (untimed),
+    # which walks like the reference (its node counts are the byte basis); a second instrumented
+    # pass walks speculatively like the timed kernel (CRT_COUNT_SPEC=1, read at the call) for the
+    # timed kernel's phase shares and lane utilization
     cnt = scene.render_count(local, cam, tiling)
+    os.environ["CRT_COUNT_SPEC"] = "1"
+    try:
+        cnt_spec = scene.render_count(local, cam, tiling)
+    finally:
+        del os.environ["CRT_COUNT_SPEC"]
     alg_bytes = (cnt.nodes_visited * NODE_B + cnt.sphere_tests * SPHERE_B + cnt.parallelogram_tests * QUAD_B
                  + len(owned) * w * PIXEL_B)
     rays_per_sample = cnt.rays / max(1, cnt.samples)
@@ -436,12 +444,18 @@ def main() -> int:
                      "peak_tflops": FP64_VECTOR_PEAK_TFLOPS, "rays_per_sample": round(rays_per_sample, 4),
                      "nodes_per_ray": round(cnt.nodes_visited / max(1, cnt.rays), 3),
                      "prim_tests_per_ray": round((cnt.sphere_tests + cnt.parallelogram_tests) / max(1, cnt.rays), 3)},
-            # per-phase shares and lane utilization of the instrumented pass, which walks like
-            # the reference (no speculative walk) so that its node counts are the byte basis
-            "instrumented_pass": "plain walk (reference node-test counts); timed kernel walks speculatively",
-            "wave_time_share": {k: round(getattr(cnt, "ticks_" + k) / max(1, cnt.ticks_total), 4)
+            # per-phase shares and lane utilization of the two instrumented passes: the timed
+            # kernel's (speculative walk) and the reference-like one (plain walk, whose node
+            # counts are the byte basis)
+            "instrumented_pass": {"timed_walk": "speculative walk, as the timed kernel (CRT_COUNT_SPEC=1)",
+                                  "plain_walk": "reference node-test sequence (algorithmic-byte basis)"},
+            "wave_time_share": {k: round(getattr(cnt_spec, "ticks_" + k) / max(1, cnt_spec.ticks_total), 4)
                                 for k in ("walk", "leaf", "shade", "tail")},
             "lane_utilization": {
+                "walk": round(cnt_spec.nodes_visited / max(1, 64 * cnt_spec.wave_iters_walk), 4),
+                "leaf": round((cnt_spec.sphere_tests + cnt_spec.parallelogram_tests) / max(1, 64 * cnt_spec.wave_iters_leaf), 4),
+                "shade": round(cnt_spec.rays / max(1, 64 * cnt_spec.wave_iters_shade), 4)},
+            "lane_utilization_plain_walk": {
                 "walk": round(cnt.nodes_visited / max(1, 64 * cnt.wave_iters_walk), 4),
                 "leaf": round((cnt.sphere_tests + cnt.parallelogram_tests) / max(1, 64 * cnt.wave_iters_leaf), 4),
                 "shade": round(cnt.rays / max(1, 64 * cnt.wave_iters_shade), 4)},

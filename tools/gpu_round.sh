@@ -10,7 +10,7 @@
 #   7. PMC passes of configs 3 and 4 (PMC_CONFIGS=1)     -> gpurun_out/pmc_c3, pmc_c4
 #   8. VALU issue-cost microbenchmark (VALU_RATE=1)      -> gpurun_out/valu_rate.json
 #   9. bench lines of BASELINE configs 3, 4, 5 on one GPU (CONFIGS="3 4 5") -> gpurun_out/bench_config<c>.json
-# SKIP_TESTS=1 skips 1-2; SKIP_PMC=1 skips 5-6; STEPS sets the bench steps.
+# SKIP_TESTS=1 skips 1-2; SKIP_BENCH=1 skips 3-4; SKIP_PMC=1 skips 5-6; STEPS sets the bench steps.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R"
@@ -50,10 +50,12 @@ step_valu() {
   [ -n "$VALU_RATE" ] || return 0
   timeout -k 10 120 tools/build/valu_rate > gpurun_out/valu_rate.json && echo "valu_rate ok"
 }
-step_tests &&
-timeout -k 10 600 python bench.py --steps $STEPS --warmup 2 > gpurun_out/bench.json 2> gpurun_out/bench.err && echo "bench ok" &&
-(cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof" -o run --output-format csv -- python3 "$R/bench.py" --steps $STEPS --warmup 2 --no-cpu-baseline > "$R/gpurun_out/bench_prof.json" 2> "$R/gpurun_out/bench_prof.err") && echo "rocprof ok" &&
-step_pmc && step_configs && step_valu && step_bench_configs
+step_bench() {
+  [ -n "$SKIP_BENCH" ] && return 0
+  timeout -k 10 600 python bench.py --steps $STEPS --warmup 2 > gpurun_out/bench.json 2> gpurun_out/bench.err && echo "bench ok" &&
+  (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof" -o run --output-format csv -- python3 "$R/bench.py" --steps $STEPS --warmup 2 --no-cpu-baseline > "$R/gpurun_out/bench_prof.json" 2> "$R/gpurun_out/bench_prof.err") && echo "rocprof ok"
+}
+step_tests && step_bench && step_pmc && step_configs && step_valu && step_bench_configs
 rc=$?
 cat gpurun_out/bench.json 2>/dev/null
 grep -h "render_kernel\|resolve" gpurun_out/prof/*kernel_stats.csv 2>/dev/null | head -4
