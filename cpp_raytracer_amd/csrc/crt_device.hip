@@ -1101,7 +1101,10 @@ __device__ __forceinline__ void walk(const SceneView& S, Stack<SE>& st, const do
 // the entered leaf's primitives in order (bvh.h:635-652), then "return" to the DFS.
 // Sphere-only scenes store spheres in slot order, so the slot indexes them directly and the next
 // sphere is loaded while the current one is tested.
-template <typename SE, bool COUNT, bool TOP, bool LS, bool FAST = false>
+// QONLY: every primitive is a parallelogram (the flat-parallelogram instances): the sphere paths,
+// and with them the ray's sphere constants (dot(d, d), its reciprocal, the coarse-reject limits),
+// are compiled out
+template <typename SE, bool COUNT, bool TOP, bool LS, bool FAST = false, bool QONLY = false>
 __device__ __forceinline__ void leaf_step(const SceneView& S, Stack<SE>& st, const double o[3],
                                               const double d[3], double tmin, float tmin32, bool sphere_only, bool pairs,
                                               bool qfilter, bool qflat, Trav& R, LaneCounters& ctr) {
@@ -1109,7 +1112,7 @@ __device__ __forceinline__ void leaf_step(const SceneView& S, Stack<SE>& st, con
     const uint32_t end = range.x + range.y;
     const double ia = recip_a<FAST>(R.a), lo = lim_tmin(tmin, R.a);
     double hi = lim_tmax(R.tmax, R.a);
-    if (pairs && range.y <= 32 && leaf_ray32_ok(o, d, R.a)) {
+    if (!QONLY && pairs && range.y <= 32 && leaf_ray32_ok(o, d, R.a)) {
         // two passes: the packed f32 candidate filter over every sphere against the leaf-entry
         // t_max, then the full test of the candidates in slot order with the shrinking t_max. A
         // sphere the first pass rejects is rejected by the full test for any smaller t_max too,
@@ -1225,7 +1228,7 @@ __device__ __forceinline__ void leaf_step(const SceneView& S, Stack<SE>& st, con
                 R.found = true;
             }
         }
-    } else if (sphere_only) {
+    } else if (!QONLY && sphere_only) {
         DevSphere cur = sphere_at<LS>(S, range.x);
         for (uint32_t i = range.x; i < end; ++i) {
             // one past the leaf's last sphere is still inside the scene copy (sphere_mat follows
@@ -1252,7 +1255,7 @@ __device__ __forceinline__ void leaf_step(const SceneView& S, Stack<SE>& st, con
             double t;
             bool h;
             if (COUNT && wave_leader()) ctr.it_leaf++;
-            if (ref & kRefQuad) {
+            if (QONLY || (ref & kRefQuad)) {
                 if (COUNT) ctr.quad_tests++;
                 if constexpr (LS) h = hit_quad(lds_rec<DevQuad>(S.quads_lds + ((ref & ~kRefQuad) << 7)), o, d, tmin, R.tmax, t);
                 else h = hit_quad(S.quads[ref & ~kRefQuad], o, d, tmin, R.tmax, t);
@@ -1696,7 +1699,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W5 ? kMa
                 if (wave_leader()) atomicAdd(&counters->round_leaves, nl);
             }
             if (COUNT) cl -= static_cast<uint32_t>(wall_clock64());
-            if (R.state == kLeaf) leaf_step<SE, COUNT, kTopTreelet && !LSCENE, LSCENE, kFast>(S, st, P.o, P.d, C.t_min, tmin32, kSphOnly || (!kFlatOnly && W.sphere_only != 0), !kFlatOnly && W.spheres_f32 != 0, kFlatOnly || (!kSphOnly && W.quads_f32 != 0), kFlatOnly || (!kSphOnly && W.quads_flat != 0), R, ctr);
+            if (R.state == kLeaf) leaf_step<SE, COUNT, kTopTreelet && !LSCENE, LSCENE, kFast, kFlatOnly>(S, st, P.o, P.d, C.t_min, tmin32, kSphOnly || (!kFlatOnly && W.sphere_only != 0), !kFlatOnly && W.spheres_f32 != 0, kFlatOnly || (!kSphOnly && W.quads_f32 != 0), kFlatOnly || (!kSphOnly && W.quads_flat != 0), R, ctr);
             if (COUNT) cl += static_cast<uint32_t>(wall_clock64());
             const uint64_t pending = __ballot(R.state == kWalk);
             const uint64_t finished = __ballot(R.state == kDone);
