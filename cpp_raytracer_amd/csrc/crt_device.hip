@@ -888,10 +888,31 @@ typedef __attribute__((address_space(3))) const NodeF LdsNodeF;
 typedef __attribute__((address_space(1))) const NodeF GlobalNodeF;
 template <bool TOP, bool LS>
 __device__ __forceinline__ void fetch_nodef(const SceneView& S, uint32_t cur, Uvec4& q0, Uvec4& q1) {
-    if (LS || (TOP && cur < S.ntop)) {
+    if (LS) {
         LdsNodeF* p = (LdsNodeF*)static_cast<uintptr_t>(cur);
         q0 = p->q0;
         q1 = p->q1;
+    } else if (TOP) {
+        // Lanes below the treelet read HBM, the others LDS, into the same registers. Written as C,
+        // the compiler waits for the HBM loads before it issues the LDS reads (it cannot know that
+        // the two exec masks are disjoint, so it orders the register writes), which puts the LDS
+        // latency behind the HBM latency in every step of a wave with lanes on both sides. Here
+        // both are in flight together, and the statement waits for both (its loads are outside
+        // the compiler's counters).
+        const uint64_t hbm = __ballot(cur >= S.ntop);
+        uint64_t save;
+        asm volatile(
+            "s_and_saveexec_b64 %[save], %[hbm]\n\t"
+            "global_load_dwordx4 %[q0], %[cur], %[base]\n\t"
+            "global_load_dwordx4 %[q1], %[cur], %[base] offset:16\n\t"
+            "s_andn2_b64 exec, %[save], %[hbm]\n\t"
+            "ds_read_b128 %[q0], %[cur]\n\t"
+            "ds_read_b128 %[q1], %[cur] offset:16\n\t"
+            "s_mov_b64 exec, %[save]\n\t"
+            "s_waitcnt vmcnt(0) lgkmcnt(0)"
+            : [q0] "=&v"(q0), [q1] "=&v"(q1), [save] "=&s"(save)
+            : [cur] "v"(cur), [hbm] "s"(hbm), [base] "s"(S.fnodes)
+            : "memory");
     } else {
         GlobalNodeF* p = (GlobalNodeF*)(reinterpret_cast<const char*>(S.fnodes) + cur);
         q0 = p->q0;
