@@ -920,6 +920,30 @@ __device__ __forceinline__ void fetch_nodef(const SceneView& S, uint32_t cur, Uv
     }
 }
 
+// The node's two words (w0, w1: bytes 24-31) alone, the same way
+typedef uint32_t Uvec2 __attribute__((ext_vector_type(2)));
+template <bool TOP, bool LS>
+__device__ __forceinline__ Uvec2 fetch_nodef_words(const SceneView& S, uint32_t cur) {
+    typedef __attribute__((address_space(3))) const Uvec2 LdsU2;
+    typedef __attribute__((address_space(1))) const Uvec2 GlobalU2;
+    if (LS) return *(LdsU2*)static_cast<uintptr_t>(cur + 24);
+    if (!TOP) return *(GlobalU2*)(reinterpret_cast<const char*>(S.fnodes) + cur + 24);
+    const uint64_t hbm = __ballot(cur >= S.ntop);
+    uint64_t save;
+    Uvec2 w;
+    asm volatile(
+        "s_and_saveexec_b64 %[save], %[hbm]\n\t"
+        "global_load_dwordx2 %[w], %[cur], %[base] offset:24\n\t"
+        "s_andn2_b64 exec, %[save], %[hbm]\n\t"
+        "ds_read_b64 %[w], %[cur] offset:24\n\t"
+        "s_mov_b64 exec, %[save]\n\t"
+        "s_waitcnt vmcnt(0) lgkmcnt(0)"
+        : [w] "=&v"(w), [save] "=&s"(save)
+        : [cur] "v"(cur), [hbm] "s"(hbm), [base] "s"(S.fnodes)
+        : "memory");
+    return w;
+}
+
 template <typename SE, bool COUNT, bool EXACT, bool TOP, bool LS, bool GS, bool SPEC>
 __device__ __forceinline__ void walk(const SceneView& S, Stack<SE>& st, const double o[3], const double d[3],
                                      double tmin, float tmin32, Trav& R, LaneCounters& ctr) {
@@ -1056,10 +1080,9 @@ __device__ __forceinline__ void walk(const SceneView& S, Stack<SE>& st, const do
         }
         // the recorded node's words (a leaf's primitive range, or the sentinel: traversal over)
         {
-            Uvec4 q0, q1;
-            fetch_nodef<TOP, LS>(S, pref, q0, q1);
-            w0 = q1.z;
-            w1 = q1.w;
+            const Uvec2 w = fetch_nodef_words<TOP, LS>(S, pref);
+            w0 = w.x;
+            w1 = w.y;
         }
         R.state = w1 == kSentinelW1 ? kDone : kLeaf;
         R.first = w0;
