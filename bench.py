@@ -414,9 +414,14 @@ def main() -> int:
     if pmc_data is None:
         roofline["note"] = "no PMC summary of this workload on this exact build: issue fraction and traffic unmeasured"
 
+    # Dielectric reflect-or-refract draws of every rendered frame (warm-up, timed, instrumented)
+    # that a one-ulp different pow() could have flipped (crt_schlick.h): 0 = every branch is the
+    # reference's whatever libm the reference is built against
+    guard = scene.guard(local)
     if distributed:
-        t = torch.tensor([alg_bytes, cnt.rays, cnt.samples, cnt.nodes_visited], dtype=torch.float64, device="cuda")
+        t = torch.tensor([alg_bytes, cnt.rays, cnt.samples, cnt.nodes_visited, guard], dtype=torch.float64, device="cuda")
         dist.all_reduce(t)  # totals for the record
+        guard = int(t[4])
     if rank == 0:
         cpu = None if args.no_cpu_baseline else cpu_baseline(args, data, log)
         out = {
@@ -464,6 +469,9 @@ def main() -> int:
                                 "candidate_wave_iters_per_filter_wave_iter": round(cnt.wave_iters_candidates / max(1, cnt.wave_iters_leaf), 4)},
             "f32_walk": {"f64_decided_node_tests": round(cnt.slow_node_tests / max(1, cnt.nodes_visited), 6),
                          "walk_iters_with_f64": round(cnt.wave_iters_slow / max(1, cnt.wave_iters_walk), 6)},
+            "schlick_guard": {"undecided_draws": guard, "frames": args.warmup + args.steps + 2,
+                              "basis": "Dielectric draws a one-ulp different pow() could flip, counted by the "
+                                       "kernel (crt_render_guard); 0 = frames bit-for-bit the reference's branches"},
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
