@@ -9,6 +9,7 @@ sizes, background), depths from 1 to 50 and, for some seeds, the whole world sca
 (CRT_NO_LDS_SCENE). Bar: the paths are bit-identical, so each channel is within 1e-12 x max(1,
 |want|) (the colour's forward vs recursive accumulation moves a few ulps, as in test_gpu_parity.py;
 north_star's 1e-4 holds a fortiori), and the Schlick guard (crt_schlick.h) at 0."""
+import os
 import sys
 
 import numpy as np
@@ -104,7 +105,8 @@ def render_gpu(crt, d, base):
     return out, guard
 
 
-@pytest.mark.parametrize("seed", range(48))
+# CRT_FUZZ_WORLDS widens the sweep for a one-off run (profiles/r04_final/fuzz_*.log)
+@pytest.mark.parametrize("seed", range(int(os.environ.get("CRT_FUZZ_WORLDS", "48"))))
 def test_random_world_matches_oracle(crt, monkeypatch, seed):
     family, d = random_world(crt, seed)
     base = 9000 + seed
