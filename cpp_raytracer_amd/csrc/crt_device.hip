@@ -20,6 +20,7 @@
 #include <string>
 #include <mutex>
 #include <thread>
+#include <type_traits>
 #include <vector>
 
 #include "crt_internal.h"
@@ -1211,18 +1212,27 @@ __device__ __forceinline__ void leaf_step(const SceneView& S, Stack<SE>& st, con
         // f32 node test on each one's flat box (crt_quad_filter.h: a rejection is a proven miss of
         // the reference's Parallelogram::hit_by for this t_max and any smaller one); rays outside
         // the walk's range have marg = inf and keep every parallelogram. Pass 2 as below.
+        // one loop per flat axis over the leaf's records grouped by it (stage_image), each record
+        // setting the bit of its slot
         uint32_t cand = 0;
-        for (uint32_t i = 0; i < range.y; ++i) {
+        const uint32_t base = S.quadf_lds + (range.x << 5);
+        const uint32_t g = lds_u32(base + 28);  // the group sizes, in the leaf's first record
+        const uint32_t e0 = g & 0xffu, e1 = e0 + ((g >> 8) & 0xffu);
+        uint32_t i = 0;
+        const auto filter = [&](auto axis) {
             if (COUNT) {
                 ctr.quad_tests++;
                 if (wave_leader()) ctr.it_leaf++;
             }
-            LdsNodeF* p = (LdsNodeF*)static_cast<uintptr_t>(S.quadf_lds + ((range.x + i) << 5));
+            LdsNodeF* p = (LdsNodeF*)static_cast<uintptr_t>(base + (i << 5));
             const Uvec4 q0 = p->q0, q1 = p->q1;
             const float b[6] = {__uint_as_float(q0.x), __uint_as_float(q0.y), __uint_as_float(q0.z),
                                 __uint_as_float(q0.w), __uint_as_float(q1.x), __uint_as_float(q1.y)};
-            cand |= static_cast<uint32_t>(flat_box_candidate<DevMinMax>(b, R.inv32, R.oinv32, tmin32, R.tmax32, R.marg)) << i;
-        }
+            cand |= static_cast<uint32_t>(flat_axis_candidate<decltype(axis)::value, DevMinMax>(b, R.inv32, R.oinv32, tmin32, R.tmax32, R.marg)) << q1.z;
+        };
+        for (; i < e0; ++i) filter(std::integral_constant<int, 0>{});
+        for (; i < e1; ++i) filter(std::integral_constant<int, 1>{});
+        for (; i < range.y; ++i) filter(std::integral_constant<int, 2>{});
         while (cand) {
             if (COUNT) {
                 ctr.cand++;
@@ -2081,6 +2091,40 @@ static void stage_image(crt_scene* s) {
         if (qb) quads_bad = true;
         if (fb) flat_bad = true;
     });
+    // Parallelogram-only scenes of axis-aligned parallelograms (slot = parallelogram): each
+    // leaf's flat boxes are grouped by the axis their box is flat on (x, then y, then z; slot
+    // order inside a group), each record keeps its slot's offset in the leaf (pad[0]) and the
+    // leaf's first record the group sizes (pad[1] = nx | ny << 8), so the filter runs one loop per
+    // axis with the flat axis' two slab values folded into one (leaf_step, flat_axis_candidate).
+    // The records' order only changes which iteration computes a candidate bit, not the bit.
+    if (!flat_bad && n_sp == 0 && n_q > 0) {
+        parallel_for(n_nodes, 1 << 12, [&](size_t a, size_t b) {
+            DevQuadBox tmp[32];
+            for (size_t k = a; k < b; ++k) {
+                const DevNode& nd = s->dnodes[k];
+                if (nd.count == 0 || nd.count > 32 || nd.count == kSentinelCount) continue;
+                // the pad (node 1, crt_host.cpp): an empty-box leaf over slot 0 that no node
+                // refers to; regrouping it too would race with the real leaf of slot 0
+                if (k == 1 && !(nd.b[0] <= nd.b[1])) continue;
+                uint32_t n = 0, groups[3] = {0, 0, 0};
+                for (uint32_t axis = 0; axis < 3; ++axis)
+                    for (uint32_t j = 0; j < nd.count; ++j) {
+                        const DevQuadBox& r = quadbox[nd.index + j];
+                        uint32_t flat = 3;
+                        for (uint32_t q = 0; q < 3 && flat == 3; ++q)
+                            if (r.b[2 * q] == r.b[2 * q + 1]) flat = q;
+                        if (flat == axis || (axis == 2 && flat == 3)) {
+                            tmp[n] = r;
+                            tmp[n].pad[0] = j;
+                            ++n;
+                            ++groups[axis];
+                        }
+                    }
+                tmp[0].pad[1] = groups[0] | groups[1] << 8;
+                std::memcpy(&quadbox[nd.index], tmp, nd.count * sizeof(DevQuadBox));
+            }
+        });
+    }
     // Shading constants precomputed per slot, with the reference's own operations (IEEE f64, no
     // contraction), so shade reads the values its divisions would give:
     //   emit[0] of a non-emitting sphere slot = 1 / r (the normal's (p - c) / r, vec3d.h:34);

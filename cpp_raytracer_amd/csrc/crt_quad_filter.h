@@ -230,6 +230,29 @@ CRT_HD bool flat_box_candidate(const float b[6], const float inv32[3], const flo
     return !(hi - lo < -th);
 }
 
+// flat_box_candidate for a box flat on axis K (b[2K] == b[2K + 1], so the axis' two slab values
+// are one, t): lo' = max(t, the other axes' mins, tmin') and hi' = min(t, the other axes' maxes,
+// tmax') take the min / max of the same values as flat_box_candidate's lo' / hi' (min(t, t) =
+// max(t, t) = t), in another order; min / max of non-NaN values are exact, so they are the same
+// floats and the decision is the same bit, with one FMA and two min / max fewer. (A NaN arises
+// only for rays outside the walk's range, where marg = inf makes both return true.) The kernel
+// runs it over the leaf's records grouped by flat axis (crt_device.hip stage_image, leaf_step);
+// tools/fuzz_quad_filter.cpp checks it against flat_box_candidate on every flat case.
+template <int K, typename MM>
+CRT_HD bool flat_axis_candidate(const float b[6], const float inv32[3], const float oinv32[3], float tmin32,
+                                float tmax32, float marg) {
+    constexpr int I = K == 0 ? 1 : 0, J = K == 2 ? 1 : 2;
+    const float t = std::fma(b[2 * K], inv32[K], -oinv32[K]);
+    const float i0 = std::fma(b[2 * I], inv32[I], -oinv32[I]);
+    const float i1 = std::fma(b[2 * I + 1], inv32[I], -oinv32[I]);
+    const float j0 = std::fma(b[2 * J], inv32[J], -oinv32[J]);
+    const float j1 = std::fma(b[2 * J + 1], inv32[J], -oinv32[J]);
+    const float lo = MM::max3(MM::min(i0, i1), MM::min(j0, j1), MM::max_s(t, tmin32));
+    const float hi = MM::min3(MM::max(i0, i1), MM::max(j0, j1), MM::min(t, tmax32));
+    const float th = std::fma(MM::max_abs(lo, hi), 0x1p-19f, marg);
+    return !(hi - lo < -th);
+}
+
 // host min / max for flat_box_candidate
 struct HostMinMax {
     static float min(float a, float b) { return std::fmin(a, b); }

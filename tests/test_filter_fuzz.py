@@ -25,6 +25,9 @@ def test_quad_filter_never_rejects_a_hit(tmp_path):
     out = _run(tmp_path, "g++", ROOT / "tools" / "fuzz_quad_filter.cpp", "-std=c++20", 1)
     lines = [l for l in out.splitlines() if "violations" in l]
     assert len(lines) == 2 and all("violations 0;" in l for l in lines), out
+    # the kernel's per-axis form of the flat-box filter gives the same bit on every flat case
+    axis = [l for l in out.splitlines() if l.startswith("per-axis flat filter")]
+    assert len(axis) == 1 and axis[0].rstrip().endswith(" 0 differ from the flat-box filter"), out
 
 
 def test_sphere_filter_never_rejects_a_hit(tmp_path):

@@ -92,6 +92,7 @@ static void rand_dir(double s, double d[3]) {
 
 static long viol = 0, miss_total = 0, miss_rejected = 0, hits = 0, skipped = 0;
 static long fviol = 0, fmiss_total = 0, fmiss_rejected = 0, fhits = 0;
+static long axis_checked = 0, axis_diff = 0;  // flat_axis_candidate vs flat_box_candidate
 
 // the render kernel's flat-box filter for axis-aligned parallelograms (crt_device.hip leaf_step
 // calls the same crt::flat_box_candidate), with the ray constants of trav_init (inv32 =
@@ -111,7 +112,17 @@ static bool flat_candidate(const crt::DevQuadBox& b, const double o[3], const do
     }
     const float marg = f32 ? std::fmax(A * 0x1p-19f, 0x1p-60f) : INFINITY;
     const float tmin32 = static_cast<float>(tmin), tmax32 = static_cast<float>(std::fmin(tmax, 0x1p100));
-    return crt::flat_box_candidate<crt::HostMinMax>(b.b, inv, oinv, tmin32, tmax32, marg);
+    const bool c = crt::flat_box_candidate<crt::HostMinMax>(b.b, inv, oinv, tmin32, tmax32, marg);
+    // the kernel's per-axis form (grouped leaves) must give the same bit
+    int flat = -1;
+    for (int k = 0; k < 3 && flat < 0; ++k)
+        if (b.b[2 * k] == b.b[2 * k + 1]) flat = k;
+    const bool ca = flat == 0   ? crt::flat_axis_candidate<0, crt::HostMinMax>(b.b, inv, oinv, tmin32, tmax32, marg)
+                    : flat == 1 ? crt::flat_axis_candidate<1, crt::HostMinMax>(b.b, inv, oinv, tmin32, tmax32, marg)
+                                : crt::flat_axis_candidate<2, crt::HostMinMax>(b.b, inv, oinv, tmin32, tmax32, marg);
+    ++axis_checked;
+    axis_diff += flat < 0 || ca != c;
+    return c;
 }
 
 static long fwide = 0;  // flat cases outside the generic filter's range (quad_ray32_ok false)
@@ -252,5 +263,6 @@ int main(int argc, char** argv) {
     std::printf("flat-box filter (axis-aligned parallelograms): exact hits %ld, violations %ld; exact misses %ld, "
                 "rejected %.4f; %ld of them outside the generic filter's range\n", fhits, fviol, fmiss_total,
                 fmiss_total ? static_cast<double>(fmiss_rejected) / fmiss_total : 0.0, fwide);
-    return viol != 0 || fviol != 0;
+    std::printf("per-axis flat filter: %ld cases, %ld differ from the flat-box filter\n", axis_checked, axis_diff);
+    return viol != 0 || fviol != 0 || axis_diff != 0 || axis_checked == 0;
 }
