@@ -77,6 +77,7 @@ struct SceneView {
     // LSCENE kernels: LDS byte offsets of the staged refs / f64 spheres / parallelograms, read
     // through typed LDS pointers (ds_read, not flat); spheres_lds = ~0u when the spheres stay in HBM
     uint32_t refs_lds, spheres_lds, quads_lds;
+    uint32_t inv64_lds;          // flat-parallelogram LDS kernels: the lanes' 1 / d ([k][lane] doubles)
     unsigned long long* guard;   // parity guard words (DeviceCopy::guard)
 };
 
@@ -122,6 +123,7 @@ struct Work {
     uint32_t sentinel;      // the sentinel node's reference (byte offset into the f32 nodes)
     uint32_t lds_cam;       // LDS copy of the CamView (read where used: keeps it out of SGPRs)
     uint32_t lds_acc;       // five-wave instances: the lanes' pixel sums (3 x kBlock doubles)
+    uint32_t lds_inv64;     // flat-parallelogram LDS instances: the lanes' 1 / d (3 x kBlock doubles)
     uint32_t packed;        // the output holds only the owned rows (CRT_TILING_PACKED)
     // instrumented pass only (COUNT): walk speculatively like the timed kernel (CRT_COUNT_SPEC=1),
     // count per-round lane numbers (CRT_ROUND_COUNTERS=1; their atomics shift the phase timings)
@@ -877,6 +879,27 @@ __device__ __forceinline__ bool slab64(GlobalNode* p, const double o[3], const d
     return (near <= far) & (near < tmax) & (far > tmin);
 }
 
+// the same test with the lane's 1 / d read from LDS (S.inv64_lds, written by the traversal set-up
+// with the same division): the flat-parallelogram instances, whose walk decides ~28% of its
+// iterations in f64 (Cornell's box faces lie on node bounds)
+__device__ __forceinline__ bool slab64_inv(GlobalNode* p, const double o[3], uint32_t inv_lds, double tmin,
+                                           double tmax) {
+    NodeLines nd;
+    node_lines(p, nd);
+    typedef __attribute__((address_space(3))) const double LdsDoubleC;
+    uint32_t t = threadIdx.x;
+    asm volatile("" : "+v"(t));  // recomputed here, not held live across the walk
+    LdsDoubleC* q = (LdsDoubleC*)static_cast<uintptr_t>(inv_lds + t * 8);
+    const double inv[3] = {q[0], q[kBlock], q[2 * kBlock]};
+    const Dvec2 bx = nd.b[0], by = nd.b[1], bz = nd.b[2];
+    const double x0 = (bx.x - o[0]) * inv[0], x1 = (bx.y - o[0]) * inv[0];
+    const double y0 = (by.x - o[1]) * inv[1], y1 = (by.y - o[1]) * inv[1];
+    const double z0 = (bz.x - o[2]) * inv[2], z1 = (bz.y - o[2]) * inv[2];
+    const double near = fmax(fmax(fmin(x0, x1), fmin(y0, y1)), fmin(z0, z1));
+    const double far = fmin(fmin(fmax(x0, x1), fmax(y0, y1)), fmax(z0, z1));
+    return (near <= far) & (near < tmax) & (far > tmin);
+}
+
 // The 32-byte f32 node at ref `cur`: LS kernels hold all nodes in LDS at offset 0 (the LDS
 // pointer is the ref itself: render_kernel checks that its dynamic LDS starts at address 0),
 // TOP kernels the first S.ntop bytes of them; the rest is read from HBM, with a separate masked
@@ -945,7 +968,7 @@ __device__ __forceinline__ Uvec2 fetch_nodef_words(const SceneView& S, uint32_t 
     return w;
 }
 
-template <typename SE, bool COUNT, bool EXACT, bool TOP, bool LS, bool GS, bool SPEC>
+template <typename SE, bool COUNT, bool EXACT, bool TOP, bool LS, bool GS, bool SPEC, bool INVL = false>
 __device__ __forceinline__ void walk(const SceneView& S, Stack<SE>& st, const double o[3], const double d[3],
                                      double tmin, float tmin32, Trav& R, LaneCounters& ctr) {
     // Every step ends with the next node in `cur`: the near child of an entered interior node,
@@ -1059,7 +1082,8 @@ __device__ __forceinline__ void walk(const SceneView& S, Stack<SE>& st, const do
                     if (COUNT && wave_leader()) ctr.it_slow++;
                     if (unc) {
                         if (COUNT) ctr.slow_nodes++;
-                        enter = slab64(node64(S, cur), o, d, tmin, R.tmax);
+                        enter = INVL ? slab64_inv(node64(S, cur), o, S.inv64_lds, tmin, R.tmax)
+                                     : slab64(node64(S, cur), o, d, tmin, R.tmax);
                     }
                 }
                 const bool inner = enter & (w1 < kLeafFlagF);
@@ -1120,7 +1144,8 @@ __device__ __forceinline__ void walk(const SceneView& S, Stack<SE>& st, const do
                 if (COUNT && wave_leader()) ctr.it_slow++;
                 if (unc) {
                     if (COUNT) ctr.slow_nodes++;
-                    enter = slab64(node64(S, cur), o, d, tmin, R.tmax);
+                    enter = INVL ? slab64_inv(node64(S, cur), o, S.inv64_lds, tmin, R.tmax)
+                                 : slab64(node64(S, cur), o, d, tmin, R.tmax);
                 }
             }
             const bool inner = enter & (w1 < kLeafFlagF);
@@ -1620,6 +1645,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W5 ? kMa
     constexpr bool kAccLds = kFast;
     typedef __attribute__((address_space(3))) double LdsDouble;
     LdsDouble* const acc_l = (LdsDouble*)static_cast<uintptr_t>(W.lds_acc + threadIdx.x * 8);
+    // the five-wave flat-parallelogram instance keeps each ray's f64 1 / d in LDS for the walk's f64
+    // node tests (slab64_inv) instead of dividing at each one
+    constexpr bool kInvLds = kFlatOnly && LSCENE && W5;
+    S.inv64_lds = W.lds_inv64;
     if (kAccLds) {
         acc_l[0] = 0;
         acc_l[kBlock] = 0;
@@ -1719,6 +1748,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W5 ? kMa
         if (start || cont) {
             st.base[-static_cast<ptrdiff_t>(st.stride)] = static_cast<SE>(W.sentinel);
             trav_init(P.o, P.d, W.f32_ok != 0, R);
+            if (kInvLds) {  // the f64 node test's 1 / d, divided once per ray (slab64_inv)
+                uint32_t t = threadIdx.x;
+                asm volatile("" : "+v"(t));
+                LdsDouble* const inv_l = (LdsDouble*)static_cast<uintptr_t>(W.lds_inv64 + t * 8);
+                inv_l[0] = 1 / P.d[0];
+                inv_l[kBlock] = 1 / P.d[1];
+                inv_l[2 * kBlock] = 1 / P.d[2];
+            }
             if (COUNT) ctr.rays++;
         }
         start = false;
@@ -1739,9 +1776,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W5 ? kMa
             if (!W.exact_slab && __ballot(R.state == kWalk && (R.neg & kZeroDir)) == 0) {
                 if (R.state == kWalk) {
                     if (!COUNT || W.count_spec)
-                        walk<SE, COUNT, false, kTopTreelet && !LSCENE, LSCENE, GSTACK, true>(S, st, P.o, P.d, C.t_min, tmin32, R, ctr);
+                        walk<SE, COUNT, false, kTopTreelet && !LSCENE, LSCENE, GSTACK, true, kInvLds>(S, st, P.o, P.d, C.t_min, tmin32, R, ctr);
                     else
-                        walk<SE, COUNT, false, kTopTreelet && !LSCENE, LSCENE, GSTACK, false>(S, st, P.o, P.d, C.t_min, tmin32, R, ctr);
+                        walk<SE, COUNT, false, kTopTreelet && !LSCENE, LSCENE, GSTACK, false, kInvLds>(S, st, P.o, P.d, C.t_min, tmin32, R, ctr);
                 }
             } else {
                 if (R.state == kWalk) walk<SE, COUNT, true, kTopTreelet && !LSCENE, LSCENE, GSTACK, false>(S, st, P.o, P.d, C.t_min, tmin32, R, ctr);
@@ -2273,6 +2310,7 @@ static uint32_t count_owned(uint32_t h, uint32_t rb, uint32_t tc, uint32_t ti) {
 static size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
 
 constexpr size_t kAccBytes = 3 * dev::kBlock * sizeof(double);  // five-wave sphere-only pixel sums
+constexpr size_t kInvBytes = 3 * dev::kBlock * sizeof(double);  // flat-parallelogram instances' 1 / d
 constexpr size_t kLdsSceneBudget = 40 * 1024 * dev::kBlock / 256;  // scene + stack per block (4 blocks of 256 a CU)
 // sphere-only LDS scenes also stage the f64 spheres (pass 2's exact tests, shading) when the block
 // still fits 40 KB: rtow 40.6 KB, 84.7 vs 85.4 ms with them in HBM / L1 (v12; round 1's layout,
@@ -2298,6 +2336,10 @@ static int launch_render(const crt_scene* s, int device, const crt_camera* cam, 
     if (W5 && PM == 0) {  // then the pixel sums (render_kernel: kAccLds)
         W.lds_acc = static_cast<uint32_t>(align16(lds));
         lds = W.lds_acc + kAccBytes;
+    }
+    if (LSCENE && PM == 2 && W5) {  // or the rays' f64 1 / d (render_kernel: kInvLds)
+        W.lds_inv64 = static_cast<uint32_t>(align16(lds));
+        lds = W.lds_inv64 + kInvBytes;
     }
     constexpr int kThreads = dev::kBlock;
     const void* kfn = reinterpret_cast<const void*>(dev::render_kernel<SE, GSTACK, LSCENE, false, PM, W5>);
@@ -2512,7 +2554,8 @@ static int dispatch_render(const crt_scene* s, int device, const crt_camera* cam
         // 3 116.5 vs 100.6 ms).
         const size_t budget5 = 160 * 1024 * dev::kBlock / (64 * dev::kManyWaves * 4);  // LDS a block at five waves a SIMD
         const bool w5 = (64 * dev::kManyWaves * 4) % dev::kBlock == 0 && (W.sphere_only || W.quads_flat) && std::getenv("CRT_FOUR_WAVES") == nullptr &&
-                        stack_at(scene_bytes) + stack_bytes + cam_bytes + (W.sphere_only ? kAccBytes : 0) <= budget5;
+                        stack_at(scene_bytes) + stack_bytes + cam_bytes + (W.sphere_only ? kAccBytes : 0) +
+                            (W.quads_flat ? kInvBytes : 0) <= budget5;
         const size_t budget = w5 ? budget5 : kLdsSceneBudget;
         const uint32_t sph64 = static_cast<uint32_t>(s->spheres.size() * sizeof(DevSphere));
         if (W.spheres_f32 && stack_at(scene_bytes + sph64) + stack_bytes + cam_bytes + (w5 ? kAccBytes : 0) <= budget)
