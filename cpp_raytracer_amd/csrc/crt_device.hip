@@ -1647,7 +1647,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W5 ? kMa
     LdsDouble* const acc_l = (LdsDouble*)static_cast<uintptr_t>(W.lds_acc + threadIdx.x * 8);
     // the five-wave flat-parallelogram instance keeps each ray's f64 1 / d in LDS for the walk's f64
     // node tests (slab64_inv) instead of dividing at each one
-    constexpr bool kInvLds = kFlatOnly && LSCENE && W5;
+    constexpr bool kInvLds = (kFlatOnly && LSCENE && W5) || (!LSCENE && !GSTACK);
     S.inv64_lds = W.lds_inv64;
     if (kAccLds) {
         acc_l[0] = 0;
@@ -2337,7 +2337,7 @@ static int launch_render(const crt_scene* s, int device, const crt_camera* cam, 
         W.lds_acc = static_cast<uint32_t>(align16(lds));
         lds = W.lds_acc + kAccBytes;
     }
-    if (LSCENE && PM == 2 && W5) {  // or the rays' f64 1 / d (render_kernel: kInvLds)
+    if ((LSCENE && PM == 2 && W5) || (!LSCENE && !GSTACK)) {  // or the rays' f64 1 / d (render_kernel: kInvLds)
         W.lds_inv64 = static_cast<uint32_t>(align16(lds));
         lds = W.lds_inv64 + kInvBytes;
     }
@@ -2580,7 +2580,7 @@ static int dispatch_render(const crt_scene* s, int device, const crt_camera* cam
         return no_top ? 0u : static_cast<uint32_t>(std::min(all_nodes, room / sizeof(DevNodeF) * sizeof(DevNodeF)));
     };
     if (stack_bytes <= kLdsStackBudget && std::getenv("CRT_FORCE_GSTACK") == nullptr) {
-        const size_t taken = stack_bytes + 2 * level;
+        const size_t taken = stack_bytes + 2 * level + kInvBytes;
         const size_t room = per_block > taken ? per_block - taken : 0;
         W.ntop = top_bytes(room);
         W.lds_nodes = 0;
