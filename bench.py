@@ -28,9 +28,11 @@ Prints ONE JSON line on rank 0 (see the repo contract), with
                 (FETCH_SIZE x2 + WRITE_SIZE) / kernel time against the 8 TB/s peak.
   cpu_baseline: the reference's own Camera::render (oracle/_ref, built from the reference
                 sources) on the host, as BASELINE.md §3 specifies: the same frame (config 2
-                whole, 500 spp), threads = every CPU this process may use, median of 3 runs; CPU
-                model and host CPU count reported, and a secondary one-run figure on the GPU's CPU
-                share (OMP_NUM_THREADS) beside it.
+                whole, 500 spp; configs 3-5 at a reduced --cpu-spp, extrapolated linearly in
+                samples and labelled so), threads = the CPUs this process is granted (usable CPUs
+                capped at the cgroup CPU quota: 16 on the GPU box), median of 3 runs; CPU model,
+                host CPU count and quota reported, and an oversubscribed one-run figure (every
+                affinity CPU a thread) beside it, labelled secondary.
 """
 from __future__ import annotations
 
@@ -56,17 +58,31 @@ SCENE_DATA = {
 }
 
 
-def kernel_source_sha() -> str:
-    """Hash of the kernel sources and of the library's compile-time switches (crt_build_info): a
-    PMC summary (profiles/pmc_latest.json) is used only when it was collected on this exact
-    build."""
-    import hashlib
+def build_stamp() -> dict:
+    """The loaded library's build stamp (crt_build_info: its compile-time switches, the sha256 of
+    its sources as compiled and their git commit, '+dirty' when they were not committed)."""
     import cpp_raytracer_amd as crt
-    h = hashlib.sha256()
-    for f in ("crt_device.hip", "crt_internal.h", "crt_quad_filter.h", "crt_schlick.h"):
-        h.update((ROOT / "cpp_raytracer_amd" / "csrc" / f).read_bytes())
-    h.update(crt.lib().crt_build_info())
-    return h.hexdigest()[:16]
+    info = crt.lib().crt_build_info().decode()
+    kv = dict(x.split("=", 1) for x in info.split() if "=" in x)
+    git = kv.get("git", "none")
+    return {"build_info": info, "source_sha": kv.get("src", "unknown"), "git_commit": git.split("+")[0],
+            "git_dirty": git.endswith("+dirty") or git == "none"}
+
+
+def kernel_source_sha() -> str:
+    """Hash of the loaded library's build info (its switches and the sha of the sources it was
+    compiled from, baked in by the Makefile): a PMC summary (profiles/pmc_latest.json) is used only
+    when it was collected on this exact build."""
+    import hashlib
+    return hashlib.sha256(build_stamp()["build_info"].encode()).hexdigest()[:16]
+
+
+def pmc_summary_usable(pj: dict, workload: str) -> bool:
+    """A PMC summary describes this run's kernel only when it was collected on this exact build of
+    a committed tree (tools/gpu_pmc.sh refuses dirty builds and records the commit) for this
+    workload; a hand-edited one (sha_note) never is."""
+    return (pj.get("workload") == workload and pj.get("kernel_source_sha") == kernel_source_sha()
+            and "sha_note" not in pj and pj.get("git_dirty") is False and bool(pj.get("git_commit")))
 
 
 def cgroup_cpu_quota() -> float | None:
@@ -132,12 +148,13 @@ def parse():
     ap.add_argument("--depth", type=int, default=50)
     ap.add_argument("--base-seed", type=int, default=2024)
     ap.add_argument("--cpu-spp", type=int, default=0,
-                    help="spp of the CPU-baseline frame (0 = the benchmarked spp: BASELINE.md §3 runs config 2 whole)")
+                    help="spp of the CPU-baseline frame (0 = the benchmarked spp: BASELINE.md §3 runs config 2 "
+                         "whole; configs 3-5 run reduced spp, extrapolated linearly in samples)")
     ap.add_argument("--cpu-runs", type=int, default=3, help="CPU-baseline runs (the median is reported)")
     ap.add_argument("--cpu-threads", type=int, default=0,
-                    help="0 = every CPU this process may use (BASELINE.md §3: OMP_NUM_THREADS=nproc)")
-    ap.add_argument("--cpu-share-spp", type=int, default=250,
-                    help="spp of the secondary one-run figure on the GPU's CPU share (OMP_NUM_THREADS); 0 = skip")
+                    help="0 = the CPUs this process is granted: usable CPUs capped at the cgroup quota")
+    ap.add_argument("--cpu-share-spp", type=int, default=100,
+                    help="spp of the secondary, oversubscribed one-run figure (every affinity CPU a thread); 0 = skip")
     ap.add_argument("--launch-check", action="store_true",
                     help="ranks only join the process group and report (tests the N-rank launch on CPU)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -146,21 +163,41 @@ def parse():
     return ap.parse_args()
 
 
+def baseline_threads(args) -> tuple[int, str]:
+    """Threads of the CPU baseline: --cpu-threads, else the CPUs this process is granted: the
+    usable (affinity) CPUs, capped at the cgroup's CPU quota when there is one (on the GPU box the
+    affinity mask lists 256 CPUs but the cgroup grants 16 CPUs' worth of time: 256 threads would
+    only oversubscribe those 16)."""
+    _, _, usable = cpu_info()
+    if args.cpu_threads:
+        return args.cpu_threads, "--cpu-threads"
+    quota = cgroup_cpu_quota()
+    if quota is not None and int(quota) < usable:
+        return max(1, int(quota)), f"cgroup CPU quota {quota} (affinity lists {usable} CPUs)"
+    return usable, "usable (affinity) CPUs"
+
+
 def cpu_baseline(args, scene_data, log) -> dict | None:
-    """Reference Camera::render on the host, as BASELINE.md §3 specifies: the same frame (config 2
-    whole by default: 1200x800, 500 spp), OpenMP over every CPU this process may use, median of
-    --cpu-runs runs. A secondary one-run figure on the GPU's CPU share (OMP_NUM_THREADS, 16 on the
-    GPU box) at --cpu-share-spp is reported beside it, labelled."""
+    """The reference's own Camera::render on the host (oracle/_ref, built from the reference
+    sources; camera.h:301-303 = render<BVH>(BVH(world)), OpenMP rows, its own per-thread RNG), as
+    BASELINE.md §3 specifies: the same scene and image, threads = the CPUs this process is granted
+    (baseline_threads), median of --cpu-runs runs. With --cpu-spp below the benchmarked spp (the
+    frames of configs 3-5, BASELINE.md §3 "Coverage") the render loop's rate is measured on that
+    reduced-spp frame and extrapolated linearly in samples; the BVH build is timed apart and
+    counted once per frame. A secondary one-run figure with every affinity CPU as a thread is kept,
+    labelled, when that differs (oversubscribed)."""
     import statistics
     import cpp_raytracer_amd as crt
     from cpp_raytracer_amd import camera_with
     model, host_cpus, usable = cpu_info()
-    threads = args.cpu_threads or usable
-    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    threads, basis = baseline_threads(args)
     ref = ROOT / "oracle" / "_ref" / "ref_driver"
     runs = max(1, args.cpu_runs)
-    spp = args.cpu_spp or args.spp
-    host = {"cpu_model": model, "host_cpus": host_cpus, "usable_cpus": usable, "cgroup_cpu_quota": cgroup_cpu_quota()}
+    spp = min(args.cpu_spp or args.spp, args.spp)
+    full_samples = args.width * args.height * args.spp
+    extrapolated = spp < args.spp
+    host = {"cpu_model": model, "host_cpus": host_cpus, "usable_cpus": usable, "cgroup_cpu_quota": cgroup_cpu_quota(),
+            "threads_basis": basis}
 
     def frame(n_spp):
         return crt.SceneData(scene_data.materials, scene_data.objects,
@@ -171,31 +208,45 @@ def cpu_baseline(args, scene_data, log) -> dict | None:
         return (f"{args.scene} seed {args.seed}, {args.width}x{args.height}, {n_spp} spp, depth {args.depth}"
                 + (f"; median of {n_runs} runs" if n_runs > 1 else "; one run"))
 
+    def summary(rates, builds, kind, sample):
+        rate = statistics.median(rates)
+        build = statistics.median(builds) if builds else 0.0
+        out = {"value": round(rate, 4), "unit": "Msamples/s", "cores": threads, "kind": kind,
+               "runs": [round(x, 4) for x in rates], **host, "sample": sample,
+               "extrapolated": extrapolated}
+        if builds:
+            out["bvh_build_seconds"] = round(build, 4)
+        if extrapolated:
+            out["extrapolation"] = (f"render-loop rate of the {spp}-spp frame, linear in samples to the "
+                                    f"benchmarked {args.spp} spp (BASELINE.md §3 Coverage)")
+        out["frame_seconds"] = round(full_samples / (rate * 1e6) + build, 3)
+        return out
+
     with tempfile.TemporaryDirectory() as td:
-        def ref_rates(n_spp, n_threads, n_runs):
+        def ref_runs(n_spp, n_threads, n_runs):
             p = Path(td) / f"scene_{n_spp}.crts"
             if not p.exists():
                 frame(n_spp).save(p)
-            rates = []
+            rates, builds = [], []
             for _ in range(n_runs):
                 r = subprocess.run([str(ref), "time", str(p), str(n_threads)], capture_output=True, text=True,
                                    timeout=900, check=True)
                 j = json.loads(r.stdout.strip().splitlines()[-1])
                 rates.append(j["samples"] / j["seconds"] / 1e6)
-            return rates
+                builds.append(j.get("build_seconds", 0.0))
+            return rates, builds
 
         if ref.exists():
             try:
-                rates = ref_rates(spp, threads, runs)
-                out = {"value": round(statistics.median(rates), 4), "unit": "Msamples/s", "cores": threads,
-                       "kind": "reference", "runs": [round(x, 4) for x in rates], **host,
-                       "sample": desc(spp, runs) + " (reference Camera::render, OpenMP, own per-thread RNG)"}
-                if share and share != threads and args.cpu_share_spp:
-                    r2 = ref_rates(args.cpu_share_spp, share, 1)
-                    out["gpu_cpu_share"] = {"value": round(r2[0], 4), "unit": "Msamples/s", "cores": share,
-                                            "sample": desc(args.cpu_share_spp, 1) + " on OMP_NUM_THREADS "
-                                            "(the GPU box's CPU share for one GPU); secondary, not the baseline: "
-                                            "with a cgroup quota below usable_cpus, usable_cpus threads oversubscribe it"}
+                rates, builds = ref_runs(spp, threads, runs)
+                out = summary(rates, builds, "reference",
+                              desc(spp, runs) + " (reference render<BVH>(BVH(world)), OpenMP, own per-thread RNG)")
+                if usable > threads and args.cpu_share_spp:
+                    r2, _ = ref_runs(min(args.cpu_share_spp, spp), usable, 1)
+                    out["oversubscribed"] = {
+                        "value": round(r2[0], 4), "unit": "Msamples/s", "cores": usable,
+                        "sample": desc(min(args.cpu_share_spp, spp), 1) + f" with {usable} threads (every "
+                        "affinity CPU); secondary, not the baseline: the cgroup grants fewer CPUs' time"}
                 return out
             except Exception as e:  # pragma: no cover - reported, not fatal
                 log(f"reference CPU baseline failed: {e}")
@@ -207,9 +258,7 @@ def cpu_baseline(args, scene_data, log) -> dict | None:
             for _ in range(runs):
                 secs, n = orc.time_render(d, threads, args.base_seed)
                 rates.append(n / secs / 1e6)
-            return {"value": round(statistics.median(rates), 4), "unit": "Msamples/s", "cores": threads,
-                    "kind": "port", "runs": [round(x, 4) for x in rates], **host,
-                    "sample": desc(spp, runs) + " (oracle C restatement, OpenMP)"}
+            return summary(rates, [], "port", desc(spp, runs) + " (oracle C restatement, OpenMP)")
         except Exception as e:  # pragma: no cover
             log(f"port CPU baseline failed: {e}")
     return None
@@ -366,15 +415,17 @@ def main() -> int:
     # counters of the timed kernel from the rocprofv3 PMC passes (tools/gpu_pmc.sh +
     # tools/pmc_summary.py) of this workload on this exact build
     pmc_data, pmc_src = None, None
-    pmc = Path(args.pmc_json)
-    if pmc.exists() and world == 1:
+    # --pmc-json first, then the per-config summaries beside it (profiles/pmc_c<k>.json)
+    pmc_paths = [Path(args.pmc_json)] + sorted(Path(args.pmc_json).parent.glob("pmc_c*.json"))
+    for pmc in pmc_paths if world == 1 else []:
         try:
             pj = json.loads(pmc.read_text())
-            if pj.get("workload") == workload and pj.get("kernel_source_sha") == kernel_source_sha():
-                pmc_data = pj
-                pmc_src = str(pmc.relative_to(ROOT)) if pmc.is_relative_to(ROOT) else str(pmc)
         except Exception:
-            pmc_data = None
+            continue
+        if pmc_summary_usable(pj, workload):
+            pmc_data = pj
+            pmc_src = str(pmc.relative_to(ROOT)) if pmc.is_relative_to(ROOT) else str(pmc)
+            break
     traffic = pmc_data.get("hbm_bytes_per_launch") if pmc_data else None
     measured_gbs = traffic / (kernel_ms * 1e-3) / 1e9 if traffic else None
     issue = pmc_data.get("valu_issue_frac") if pmc_data else None
@@ -412,7 +463,8 @@ def main() -> int:
         },
     }
     if pmc_data is None:
-        roofline["note"] = "no PMC summary of this workload on this exact build: issue fraction and traffic unmeasured"
+        roofline["note"] = ("no PMC summary of this workload on this exact committed build (tools/gpu_pmc.sh): "
+                            "issue fraction and traffic unmeasured")
 
     # Dielectric reflect-or-refract draws of every rendered frame (warm-up, timed, instrumented)
     # that a one-ulp different pow() could have flipped (crt_schlick.h): 0 = every branch is the

@@ -923,15 +923,23 @@ __device__ __forceinline__ void fetch_nodef(const SceneView& S, uint32_t cur, Uv
         // latency behind the HBM latency in every step of a wave with lanes on both sides. Here
         // both are in flight together, and the statement waits for both (its loads are outside
         // the compiler's counters).
+        // A side whose mask is empty is branched over: a vector-memory instruction issued with
+        // EXEC = 0 still takes its slot in the address / data units (TA / TD, config 4's
+        // binding resource), and a wave whose lanes are all in the treelet (or all below it)
+        // is common at the start (end) of its rays' traversals.
         const uint64_t hbm = __ballot(cur >= S.ntop);
         uint64_t save;
         asm volatile(
             "s_and_saveexec_b64 %[save], %[hbm]\n\t"
+            "s_cbranch_execz 1f\n\t"
             "global_load_dwordx4 %[q0], %[cur], %[base]\n\t"
-            "global_load_dwordx4 %[q1], %[cur], %[base] offset:16\n\t"
+            "global_load_dwordx4 %[q1], %[cur], %[base] offset:16\n"
+            "1:\n\t"
             "s_andn2_b64 exec, %[save], %[hbm]\n\t"
+            "s_cbranch_execz 2f\n\t"
             "ds_read_b128 %[q0], %[cur]\n\t"
-            "ds_read_b128 %[q1], %[cur] offset:16\n\t"
+            "ds_read_b128 %[q1], %[cur] offset:16\n"
+            "2:\n\t"
             "s_mov_b64 exec, %[save]\n\t"
             "s_waitcnt vmcnt(0) lgkmcnt(0)"
             : [q0] "=&v"(q0), [q1] "=&v"(q1), [save] "=&s"(save)
@@ -957,9 +965,13 @@ __device__ __forceinline__ Uvec2 fetch_nodef_words(const SceneView& S, uint32_t 
     Uvec2 w;
     asm volatile(
         "s_and_saveexec_b64 %[save], %[hbm]\n\t"
-        "global_load_dwordx2 %[w], %[cur], %[base] offset:24\n\t"
+        "s_cbranch_execz 1f\n\t"
+        "global_load_dwordx2 %[w], %[cur], %[base] offset:24\n"
+        "1:\n\t"
         "s_andn2_b64 exec, %[save], %[hbm]\n\t"
-        "ds_read_b64 %[w], %[cur] offset:24\n\t"
+        "s_cbranch_execz 2f\n\t"
+        "ds_read_b64 %[w], %[cur] offset:24\n"
+        "2:\n\t"
         "s_mov_b64 exec, %[save]\n\t"
         "s_waitcnt vmcnt(0) lgkmcnt(0)"
         : [w] "=&v"(w), [save] "=&s"(save)
@@ -1944,6 +1956,18 @@ __global__ __launch_bounds__(256) void ppm8_kernel(const double* __restrict__ rg
     for (int k = 0; k < 3; ++k) out[3 * i + k] = ok ? static_cast<uint8_t>(q[k]) : 0;
 }
 
+// The f64 values of the pixels ppm8_kernel listed for the host (redo = [count, pixel...]),
+// gathered into one compact buffer: the host then copies them in one transfer
+__global__ __launch_bounds__(256) void redo_gather_kernel(const double* __restrict__ rgb,
+                                                          const uint32_t* __restrict__ list, uint32_t n,
+                                                          double* __restrict__ out) {
+    const uint32_t j = blockIdx.x * 256 + threadIdx.x;
+    if (j >= n) return;
+    const size_t i = list[j];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) out[3 * static_cast<size_t>(j) + k] = rgb[3 * i + k];
+}
+
 // Closest-hit queries (BVH::hit_by for an arbitrary ray batch).
 __global__ __launch_bounds__(kBlock) void hits_kernel(SceneView S, const double* __restrict__ rays,
                                                       uint32_t n, double t_min, double t_max,
@@ -2134,6 +2158,10 @@ static void stage_image(crt_scene* s) {
     // leaf's first record the group sizes (pad[1] = nx | ny << 8), so the filter runs one loop per
     // axis with the flat axis' two slab values folded into one (leaf_step, flat_axis_candidate).
     // The records' order only changes which iteration computes a candidate bit, not the bit.
+    // A record flat on no axis cannot occur here (quad_flat_box accepted every parallelogram, so
+    // each box is flat on one axis); should one appear, the scene leaves the flat-box filter
+    // rather than have flat_axis_candidate read a wrong axis.
+    std::atomic<bool> regroup_bad{false};
     if (!flat_bad && n_sp == 0 && n_q > 0) {
         parallel_for(n_nodes, 1 << 12, [&](size_t a, size_t b) {
             DevQuadBox tmp[32];
@@ -2150,13 +2178,15 @@ static void stage_image(crt_scene* s) {
                         uint32_t flat = 3;
                         for (uint32_t q = 0; q < 3 && flat == 3; ++q)
                             if (r.b[2 * q] == r.b[2 * q + 1]) flat = q;
-                        if (flat == axis || (axis == 2 && flat == 3)) {
+                        if (flat == 3) regroup_bad = true;
+                        if (flat == axis) {
                             tmp[n] = r;
                             tmp[n].pad[0] = j;
                             ++n;
                             ++groups[axis];
                         }
                     }
+                if (n != nd.count) continue;  // a record flat on no axis (regroup_bad)
                 tmp[0].pad[1] = groups[0] | groups[1] << 8;
                 std::memcpy(&quadbox[nd.index], tmp, nd.count * sizeof(DevQuadBox));
             }
@@ -2196,7 +2226,7 @@ static void stage_image(crt_scene* s) {
     s->image_f32_ok = !f32_bad;
     s->image_spheres_f32_ok = !sph_bad;
     s->image_quads_f32_ok = !quads_bad;
-    s->image_quads_flat_ok = !flat_bad;
+    s->image_quads_flat_ok = !flat_bad && !regroup_bad;
     s->staged = true;
 }
 
@@ -2715,14 +2745,32 @@ int device_ppm_values(int device, const double* d_rgb, size_t n, int32_t* h_valu
             h_values[3 * p + 2] == dev::kPpmRedo)
             redo.push_back(p);
     if (redo.empty()) return CRT_OK;
-    std::vector<double> px(redo.size() > 4096 ? n * 3 : 3);
-    if (redo.size() > 4096) HIP_TRY(hipMemcpy(px.data(), d_rgb, n * 3 * sizeof(double), hipMemcpyDeviceToHost));
-    for (size_t p : redo) {
-        const double* src = px.data();
-        if (redo.size() > 4096) src += 3 * p;
-        else HIP_TRY(hipMemcpy(px.data(), d_rgb + 3 * p, 3 * sizeof(double), hipMemcpyDeviceToHost));
-        ppm_pixel_host(src, h_values + 3 * p);
+    // their f64 values: the whole frame when many, else gathered on the device (one upload of the
+    // list, one copy back)
+    const bool whole = redo.size() > 4096;
+    std::vector<double> px(whole ? n * 3 : redo.size() * 3);
+    if (whole) {
+        HIP_TRY(hipMemcpy(px.data(), d_rgb, n * 3 * sizeof(double), hipMemcpyDeviceToHost));
+    } else {
+        std::vector<uint32_t> list(redo.begin(), redo.end());
+        uint32_t* d_list = nullptr;
+        double* d_px = nullptr;
+        HIP_TRY(hipMalloc(&d_list, list.size() * sizeof(uint32_t)));
+        hipError_t ge = hipMalloc(&d_px, px.size() * sizeof(double));
+        if (ge == hipSuccess) ge = hipMemcpy(d_list, list.data(), list.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
+        if (ge == hipSuccess) {
+            hipLaunchKernelGGL(dev::redo_gather_kernel, dim3(static_cast<uint32_t>((list.size() + 255) / 256)), dim3(256), 0,
+                               st, d_rgb, d_list, static_cast<uint32_t>(list.size()), d_px);
+            ge = hipGetLastError();
+        }
+        if (ge == hipSuccess) ge = hipStreamSynchronize(st);
+        if (ge == hipSuccess) ge = hipMemcpy(px.data(), d_px, px.size() * sizeof(double), hipMemcpyDeviceToHost);
+        (void)hipFree(d_list);
+        if (d_px) (void)hipFree(d_px);
+        if (ge != hipSuccess) return fail(CRT_E_HIP, std::string("ppm redo gather: ") + hipGetErrorString(ge));
     }
+    for (size_t j = 0; j < redo.size(); ++j)
+        ppm_pixel_host(px.data() + 3 * (whole ? redo[j] : j), h_values + 3 * redo[j]);
     return CRT_OK;
 }
 
@@ -2922,9 +2970,18 @@ static int render_multi_impl(crt_scene* s, const crt_camera* cam, int num_device
             if (whole) {
                 if (hipMemcpy(rgb.data(), bufs[d], 3 * px * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess) rc = CRT_E_HIP;
             } else {
-                for (size_t j = 0; j < idx.size() && rc == CRT_OK; ++j)
-                    if (hipMemcpy(rgb.data() + 3 * j, bufs[d] + 3 * static_cast<size_t>(idx[j]), 3 * sizeof(double),
-                                  hipMemcpyDeviceToHost) != hipSuccess) rc = CRT_E_HIP;
+                // the listed pixels gathered on the device, then one copy (not one per pixel)
+                double* packed = nullptr;
+                if (hipMalloc(&packed, 3 * idx.size() * sizeof(double)) != hipSuccess) {
+                    rc = CRT_E_HIP;
+                } else {
+                    hipLaunchKernelGGL(dev::redo_gather_kernel, dim3(static_cast<uint32_t>((idx.size() + 255) / 256)), dim3(256),
+                                       0, nullptr, bufs[d], redo[d] + 1, static_cast<uint32_t>(idx.size()), packed);
+                    if (hipGetLastError() != hipSuccess ||
+                        hipMemcpy(rgb.data(), packed, 3 * idx.size() * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess)
+                        rc = CRT_E_HIP;
+                    (void)hipFree(packed);
+                }
             }
             if (rc != CRT_OK) {
                 rc = fail(CRT_E_HIP, "render: redo pixels");

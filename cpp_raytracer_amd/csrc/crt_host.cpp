@@ -1030,7 +1030,18 @@ int crt_abi_version(void) { return CRT_ABI_VERSION; }
 
 const char* crt_last_error(void) { return g_last_error.c_str(); }
 
-const char* crt_build_info(void) { return device_build_info(); }
+// the kernels' compile-time switches plus the build stamp (Makefile: the sha256 of the sources as
+// compiled and their git commit, "+dirty" when they differ from it)
+#ifndef CRT_SOURCE_SHA
+#define CRT_SOURCE_SHA "unknown"
+#endif
+#ifndef CRT_GIT
+#define CRT_GIT "none"
+#endif
+const char* crt_build_info(void) {
+    static const std::string info = std::string(device_build_info()) + " src=" CRT_SOURCE_SHA " git=" CRT_GIT;
+    return info.c_str();
+}
 
 void crt_free(void* p) { std::free(p); }
 

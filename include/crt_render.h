@@ -115,7 +115,9 @@ typedef struct crt_camera {
 /* Rows owned by one device/rank: row r is rendered iff (r / row_block) % tile_count == tile_index.
  * {1,1,0,0} (or NULL) = the whole frame. flags: CRT_TILING_PACKED = the output buffer holds only
  * the owned rows, packed in order (owned row k at offset k * image_w * 3): a rank or device then
- * allocates its share of the frame, not the whole frame. */
+ * allocates its share of the frame, not the whole frame.
+ * ABI change (round 4): this word was `reserved` before CRT_TILING_PACKED existed; any other bit
+ * set is rejected with CRT_E_INVALID, so a caller that left it uninitialised must now zero it. */
 #define CRT_TILING_PACKED 1u
 typedef struct crt_tiling {
     uint32_t row_block;

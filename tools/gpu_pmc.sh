@@ -10,6 +10,19 @@ OUT=$R/$1
 shift
 ARGS="--steps 1 --warmup 0 --no-cpu-baseline $*"
 mkdir -p "$OUT"
+# counters are only collected on a library built from committed sources: its build stamp
+# (crt_build_info: source sha + git commit, Makefile) must not be dirty, and its source sha must be
+# that of the sources in this tree (the .so was built from them)
+(cd "$R" && python -c "
+import hashlib, subprocess, sys
+from bench import build_stamp
+st = build_stamp()
+srcs = ['csrc/crt_device.hip', 'csrc/crt_bvh_gpu.hip', 'csrc/crt_host.cpp', 'csrc/crt_internal.h',
+        'csrc/crt_quad_filter.h', '../include/crt_render.h', 'csrc/crt_schlick.h']
+h = hashlib.sha256(b''.join(open('cpp_raytracer_amd/' + f, 'rb').read() for f in srcs)).hexdigest()[:16]
+ok = not st['git_dirty'] and st['source_sha'] == h
+print(('pmc: library ' if ok else 'pmc: REFUSED, library ') + st['build_info'] + ' tree src=' + h)
+sys.exit(0 if ok else 3)") || exit 3
 export TMPDIR=/tmp
 cd /tmp
 [ -s "$R/gpurun_out/counters_list.txt" ] || timeout -k 10 120 rocprofv3 -L > "$R/gpurun_out/counters_list.txt" 2>&1

@@ -9,7 +9,8 @@
 #   6. bench.py again, reading that summary              -> gpurun_out/bench_traffic.json
 #   7. PMC passes of configs 3 and 4 (PMC_CONFIGS=1)     -> gpurun_out/pmc_c3, pmc_c4
 #   8. VALU issue-cost microbenchmark (VALU_RATE=1)      -> gpurun_out/valu_rate.json
-#   9. bench lines of BASELINE configs 3, 4, 5 on one GPU (CONFIGS="3 4 5") -> gpurun_out/bench_config<c>.json
+#   9. bench lines of BASELINE configs 3, 4, 5 on one GPU (CONFIGS="3 4 5"), each with its CPU baseline
+#      at reduced spp, extrapolated               -> gpurun_out/bench_config<c>.json
 # SKIP_TESTS=1 skips 1-2; SKIP_BENCH=1 skips 3-4; SKIP_PMC=1 skips 5-6; STEPS sets the bench steps.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -32,12 +33,13 @@ step_configs() {
 step_bench_configs() {
   for c in $CONFIGS; do
     case $c in
-      3) a="$C3 --steps 2 --warmup 1" ;;
-      4) a="$C4 --seed 42 --steps 2 --warmup 1" ;;
-      5) a="--scene rtow_final --seed 42 --width 3840 --height 2160 --spp 10000 --depth 50 --steps 1 --warmup 0" ;;
+      # CPU baselines at reduced spp, extrapolated linearly in samples (BASELINE.md §3 Coverage)
+      3) a="$C3 --steps 2 --warmup 1 --cpu-spp 100" ;;
+      4) a="$C4 --seed 42 --steps 2 --warmup 1 --cpu-spp 16" ;;
+      5) a="--scene rtow_final --seed 42 --width 3840 --height 2160 --spp 10000 --depth 50 --steps 1 --warmup 0 --cpu-spp 16" ;;
       *) continue ;;
     esac
-    timeout -k 10 900 python bench.py $a --no-cpu-baseline > gpurun_out/bench_config$c.json 2> gpurun_out/bench_config$c.err &&
+    timeout -k 10 900 python bench.py $a > gpurun_out/bench_config$c.json 2> gpurun_out/bench_config$c.err &&
     echo "config $c: $(cat gpurun_out/bench_config$c.json | head -c 300)" || return 1
   done
 }

@@ -32,8 +32,10 @@ the effective clock GRBM_GUI_ACTIVE / 8 / kernel time. Issue cycles two ways:
 
 usage: python tools/pmc_summary.py <pmc dir> <out.json> [workload]
 The workload key defaults to config.workload of <dir>/bench_p1.json (the bench line of pass 1);
-the summary records bench.kernel_source_sha() (sources + build switches), so bench.py only uses
-counters collected on the build it is timing.
+the summary records bench.kernel_source_sha() (the loaded library's build info: its switches and
+the sha of the sources it was compiled from) and the git commit of that build, so bench.py only
+uses counters collected on the build it is timing; a library built from uncommitted sources is
+refused (tools/gpu_pmc.sh checks before collecting, this script again).
 """
 import csv
 import json
@@ -43,7 +45,7 @@ from collections import defaultdict
 from pathlib import Path
 
 sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
-from bench import kernel_source_sha  # noqa: E402
+from bench import build_stamp, kernel_source_sha  # noqa: E402
 
 TIMED = re.compile(r"render_kernel<([^,]+), (true|false), (true|false), false,")
 
@@ -72,8 +74,12 @@ def main():
     if not vals:
         raise SystemExit(f"no timed render_kernel rows under {src}")
     avg = {k: sum(v) / len(v) for k, v in vals.items()}
+    stamp = build_stamp()
+    if stamp["git_dirty"]:
+        raise SystemExit(f"library built from uncommitted sources ({stamp['build_info']}): not summarised")
     res = {"workload": workload, "kernel": names.pop(), "kernel_source_sha": kernel_source_sha(),
-           "launches": {k: len(v) for k, v in vals.items()}}
+           "git_commit": stamp["git_commit"], "git_dirty": False, "source_sha": stamp["source_sha"],
+           "build_info": stamp["build_info"], "launches": {k: len(v) for k, v in vals.items()}}
     if durs:
         res["kernel_ns_under_pmc"] = sum(durs) / len(durs)
     res.update({k: avg[k] for k in sorted(avg)})
