@@ -183,6 +183,28 @@ __device__ __forceinline__ bool wave_leader() {
     return (threadIdx.x & 63) == static_cast<uint32_t>(__ffsll(static_cast<long long>(m)) - 1);
 }
 
+// Debug builds only (-DCRT_WATCHDOG=1, never the library's default): every wave-level loop of
+// the render kernel checks a deadline (3 s after the launch's first wave started) and, past it,
+// the wave prints where it was and ends (s_endpgm), so a kernel that would spin forever finishes
+// with a report instead of hanging the device (tools/gpu_watchdog.sh).
+#ifndef CRT_WATCHDOG
+#define CRT_WATCHDOG 0
+#endif
+#if CRT_WATCHDOG
+__device__ unsigned long long crt_wd_deadline;
+#define CRT_WD(id, a, b)                                                                                   \
+    do {                                                                                                   \
+        if (wall_clock64() > *(volatile unsigned long long*)&crt_wd_deadline) {                            \
+            if (wave_leader())                                                                             \
+                printf("crt watchdog: block %u wave %u loop %d a %u b %u\n", blockIdx.x, threadIdx.x >> 6,  \
+                       (int)(id), (unsigned)(a), (unsigned)(b));                                            \
+            __builtin_amdgcn_endpgm();                                                                     \
+        }                                                                                                  \
+    } while (0)
+#else
+#define CRT_WD(id, a, b) do {} while (0)
+#endif
+
 // ---- reference RNG (rand_util.h:85-117) with per-sample state ------------------------------
 __device__ __forceinline__ double rnd(uint32_t& s, double lo, double hi) {
     s = 1664525u * s + 1013904223u;
@@ -1068,6 +1090,7 @@ __device__ __forceinline__ void walk(const SceneView& S, Stack<SE>& st, const do
         bool run = true, nopend = true;
         uint32_t pref = ~0u, pcur = 0;
         do {
+            CRT_WD(4, cur, static_cast<uint32_t>(tp - empty));
             if (run) {
                 Uvec4 q0, q1;
                 fetch_nodef<TOP, LS>(S, cur, q0, q1);
@@ -1129,6 +1152,7 @@ __device__ __forceinline__ void walk(const SceneView& S, Stack<SE>& st, const do
         return;
     } else {
         do {
+            CRT_WD(5, cur, static_cast<uint32_t>(tp - empty));
             Uvec4 q0, q1;
             fetch_nodef<TOP, LS>(S, cur, q0, q1);
             w0 = q1.z;
@@ -1227,6 +1251,7 @@ __device__ __forceinline__ void leaf_step(const SceneView& S, Stack<SE>& st, con
         }
         cand &= ~(range.y & 1u);  // an odd count's last verdict is the slot after the leaf
         while (cand) {
+            CRT_WD(6, cand, range.y);
             if (COUNT) {
                 ctr.cand++;
                 if (wave_leader()) ctr.it_cand++;
@@ -1271,6 +1296,7 @@ __device__ __forceinline__ void leaf_step(const SceneView& S, Stack<SE>& st, con
         for (; i < e1; ++i) filter(std::integral_constant<int, 1>{});
         for (; i < range.y; ++i) filter(std::integral_constant<int, 2>{});
         while (cand) {
+            CRT_WD(6, cand, range.y);
             if (COUNT) {
                 ctr.cand++;
                 if (wave_leader()) ctr.it_cand++;
@@ -1302,6 +1328,7 @@ __device__ __forceinline__ void leaf_step(const SceneView& S, Stack<SE>& st, con
             cand |= static_cast<uint32_t>(quad_candidate(q, L, [](float x) { return __builtin_amdgcn_rcpf(x); })) << i;
         }
         while (cand) {
+            CRT_WD(6, cand, range.y);
             if (COUNT) {
                 ctr.cand++;
                 if (wave_leader()) ctr.it_cand++;
@@ -1622,6 +1649,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W5 ? kMa
     // The camera constants are read from an LDS copy in start_path / shade: held in SGPRs for
     // the whole kernel they would spill (into VGPR lanes, reloaded with v_readlane per use).
     if (threadIdx.x == 0) *reinterpret_cast<CamView*>(smem + W.lds_cam) = C;
+#if CRT_WATCHDOG
+    if (threadIdx.x == 0) atomicCAS(&crt_wd_deadline, 0ull, wall_clock64() + 300000000ull);  // 3 s at 100 MHz
+#endif
     __syncthreads();
     const CamView& CL = *reinterpret_cast<const CamView*>(smem + W.lds_cam);
     const float tmin32 = W.tmin32;  // a kernel argument (SGPR): no conversion in the walk loop
@@ -1674,12 +1704,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W5 ? kMa
     uint32_t cd = 0, ci = 0;
     unsigned long long t_first_idle = 0;
     while (true) {
+        CRT_WD(1, item_pos, item_units);
         // lanes without a unit draw until each holds a unit with samples to trace or the queue
         // is dry. A unit off the image has no pixel sum; one with max_depth == 0 sums
         // RGB::zero() (camera.h:211-213) and is written at once.
         if (COUNT) cd -= static_cast<uint32_t>(wall_clock64());
         set_prio<kPrioInit>();
         while (true) {
+            CRT_WD(2, item_pos, item_units);
             const uint64_t m = __ballot(need);
             if (m == 0) break;
             if (item_pos >= item_units) {  // the item is used up: the next one from a queue
@@ -1776,6 +1808,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W5 ? kMa
         // traversal rounds (walk to the next entered leaf, test it) until enough lanes hold a
         // finished ray, or none is traversing
         while (true) {
+            CRT_WD(3, R.state, R.cur);
             if (COUNT && W.round_counters) {
                 const unsigned long long nw = __popcll(__ballot(R.state == kWalk));
                 if (wave_leader()) {
@@ -2482,6 +2515,13 @@ static int launch_render(const crt_scene* s, int device, const crt_camera* cam, 
             // keep one queue (config 2: 88.5 vs 89.0 ms with eight). CRT_XCD_QUEUES=0/1 forces.
             W.segments = knob("CRT_XCD_QUEUES", LSCENE ? 0 : 1) ? 8u : 1u;
             HIP_TRY(hipMemsetAsync(queue, 0, 8 * sizeof(uint32_t), stream));
+#if CRT_WATCHDOG
+            {
+                void* wd = nullptr;
+                HIP_TRY(hipGetSymbolAddress(&wd, HIP_SYMBOL(dev::crt_wd_deadline)));
+                HIP_TRY(hipMemsetAsync(wd, 0, sizeof(unsigned long long), stream));
+            }
+#endif
             if (count) {
                 hipLaunchKernelGGL((dev::render_kernel<SE, GSTACK, LSCENE, true, PM, W5>), dim3(static_cast<uint32_t>(blocks)),
                                    dim3(dev::kBlock), lds, stream, S, C, W, partial, gstack, ctr);
@@ -2566,9 +2606,15 @@ static int dispatch_render(const crt_scene* s, int device, const crt_camera* cam
     W.f32_ok = s->dev[device].f32_ok ? 1u : 0u;
     W.tmin32 = static_cast<float>(cam->t_min);
     const bool force_global = std::getenv("CRT_NO_LDS_SCENE") != nullptr;
-    // LDS stacks: [data][guard level: sentinel][levels 0..depth]; walk() may also read the level
-    // below the guard, so the guard starts at least one level into the allocation
-    auto stack_at = [&](size_t data_bytes) { return static_cast<uint32_t>(std::max<size_t>(data_bytes, level) + level); };
+    // LDS stacks: [data][guard level: sentinel][levels 0..depth]. walk() reads the level below the
+    // guard (the speculative pop at the sentinel) and, at a walk's exit after the sentinel, its
+    // stack pointer stands one level lower still: the guard starts at least two levels into the
+    // allocation, so every level the pointer reaches has a non-negative LDS address. (With one
+    // level, a 640-thread block on a small scene put that pointer at a negative address; the
+    // level count derived from it then wrapped, and the flat-parallelogram instance walked a
+    // garbage stack forever: the round-4 hang, found with -DCRT_WATCHDOG=1. Power-of-two blocks
+    // had wrapped back onto the right level by the modular arithmetic alone.)
+    auto stack_at = [&](size_t data_bytes) { return static_cast<uint32_t>(std::max<size_t>(data_bytes, 2 * level) + level); };
     if (!force_global && stack_at(scene_bytes) + stack_bytes <= kLdsSceneBudget) {
         W.lds_nodes = 0;
         W.lds_refs = W.lds_nodes + W.bytes_nodes;
@@ -3039,7 +3085,8 @@ const char* device_build_info() {
     // other build switches), and the offload target the Makefile compiled for
     return "arch=" CRT_ARCH " CRT_BLOCK=" CRT_STR(CRT_BLOCK) " CRT_TILE_W=" CRT_STR(CRT_TILE_W)
            " CRT_WAVES_PER_EU=" CRT_STR(CRT_WAVES_PER_EU) " CRT_WAVES_PER_EU_LDS=" CRT_STR(CRT_WAVES_PER_EU_LDS)
-           " CRT_SHADE_BATCH=" CRT_STR(CRT_SHADE_BATCH) " CRT_CHUNK_MIN=" CRT_STR(CRT_CHUNK_MIN);
+           " CRT_SHADE_BATCH=" CRT_STR(CRT_SHADE_BATCH) " CRT_CHUNK_MIN=" CRT_STR(CRT_CHUNK_MIN)
+           " CRT_WATCHDOG=" CRT_STR(CRT_WATCHDOG);
 }
 
 }  // namespace crt
