@@ -70,11 +70,14 @@ def build_stamp() -> dict:
 
 
 def kernel_source_sha() -> str:
-    """Hash of the loaded library's build info (its switches and the sha of the sources it was
-    compiled from, baked in by the Makefile): a PMC summary (profiles/pmc_latest.json) is used only
-    when it was collected on this exact build."""
+    """Hash of the loaded library's build info without its git field (its switches and the sha of
+    the sources it was compiled from, baked in by the Makefile): a PMC summary
+    (profiles/pmc_latest.json) is used only when it was collected on a build of these exact
+    sources; the commit is recorded beside it (and must be clean), but later commits that do not
+    touch the library's sources leave the match intact."""
     import hashlib
-    return hashlib.sha256(build_stamp()["build_info"].encode()).hexdigest()[:16]
+    info = " ".join(x for x in build_stamp()["build_info"].split() if not x.startswith("git="))
+    return hashlib.sha256(info.encode()).hexdigest()[:16]
 
 
 def pmc_summary_usable(pj: dict, workload: str) -> bool:
