@@ -188,6 +188,13 @@ class GpuScene:
     def upload(self, device: int = 0) -> None:
         check(lib().crt_scene_upload(self._h, device), f"crt_scene_upload(device={device})")
 
+    def device_image(self, device: int = 0) -> np.ndarray:
+        """The bytes of the scene's copy in HBM of `device` (crt_scene_image)."""
+        out = np.zeros(self.info().device_bytes, np.uint8)
+        check(lib().crt_scene_image(self._h, device, out.ctypes.data, out.nbytes),
+              f"crt_scene_image(device={device})")
+        return out
+
     def render_async(self, device: int, cam: Camera, out_ptr: int, stream: int = 0,
                      tiling: Optional[Tiling] = None) -> None:
         """Enqueue a render of the owned rows into the device buffer at out_ptr."""

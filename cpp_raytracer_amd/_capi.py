@@ -115,6 +115,7 @@ EXPORTS = {
     "crt_scene_info_get": (C.c_int, [C.c_void_p, P(SceneInfo)]),
     "crt_scene_export_bvh": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
     "crt_scene_upload": (C.c_int, [C.c_void_p, C.c_int]),
+    "crt_scene_image": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t]),
     "crt_scene_destroy": (None, [C.c_void_p]),
     "crt_camera_resolve": (C.c_int, [P(CameraSettings), P(Camera)]),
     "crt_render_async": (C.c_int, [C.c_void_p, C.c_int, P(Camera), P(Tiling), C.c_void_p, C.c_void_p]),

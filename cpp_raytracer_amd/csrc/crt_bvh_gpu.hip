@@ -755,23 +755,23 @@ __global__ __launch_bounds__(kThreads) void emit_preorder(const TNode* __restric
     out[pre[i]] = o;
 }
 
-// Builds s->nodes / s->order on `device` for the (non-empty, non-linear) primitive list, from the
-// primitives' boxes (6 doubles each, in primitive order); centroids, the tree and its preorder
-// numbering are computed on the device.
-int device_build_bvh(crt_scene* s, uint32_t num_buckets, uint32_t max_leaf, int device,
-                     const BigVec<double>& boxes) {
+void device_tree_free(DeviceTree& t) {
+    (void)hipFree(t.nodes);
+    (void)hipFree(t.order);
+    t.nodes = nullptr;
+    t.order = nullptr;
+}
+
+// The tree of n (> 0) primitives from their boxes in HBM of the current device (d_pb: 6 doubles
+// each, in primitive order): centroids, the levels and the preorder numbering on the device. The
+// preorder node array and the slot order stay in HBM (out.nodes / out.order, freed by
+// device_tree_free).
+int device_build_tree(size_t n, const double* d_pb, uint32_t num_buckets, uint32_t max_leaf, DeviceTree& out) {
     using namespace bvhgpu;
     if (num_buckets < 2 || num_buckets > kMaxBuckets)
         return fail(CRT_E_INVALID, "GPU BVH build supports 2..64 buckets");
-    int ndev = 0;
-    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev)
-        return fail(CRT_E_NODEVICE, "GPU BVH build: device " + std::to_string(device) + " not visible");
-    int prev = 0;
-    (void)hipGetDevice(&prev);
-    (void)hipSetDevice(device);
-    const size_t n = s->prims.size();
     int rc = CRT_OK;
-    double *d_pb = nullptr, *d_pc = nullptr;
+    double* d_pc = nullptr;
     uint32_t *d_order = nullptr, *d_f = nullptr, *d_t = nullptr, *d_ctr = nullptr;
     uint8_t* d_pred = nullptr;
     Task *d_ta = nullptr, *d_tb = nullptr;
@@ -782,7 +782,6 @@ int device_build_bvh(crt_scene* s, uint32_t num_buckets, uint32_t max_leaf, int 
     double* d_chunk_red = nullptr;
     unsigned int* d_bn = nullptr;
     unsigned long long* d_bb = nullptr;
-    BigVec<uint32_t> order(n);
     uint32_t nnodes = 0;
     std::vector<uint32_t> level_end;  // build ids [level_end[L - 1], level_end[L]) are level L
     uint32_t *d_size = nullptr, *d_pre = nullptr, *d_maxleaf = nullptr;
@@ -797,7 +796,6 @@ int device_build_bvh(crt_scene* s, uint32_t num_buckets, uint32_t max_leaf, int 
         tp = now;
     };
     {
-        BV_TRY(hipMalloc(&d_pb, n * 6 * sizeof(double)));
         BV_TRY(hipMalloc(&d_pc, n * 3 * sizeof(double)));
         BV_TRY(hipMalloc(&d_order, n * 4));
         BV_TRY(hipMalloc(&d_f, n * 4));
@@ -816,7 +814,6 @@ int device_build_bvh(crt_scene* s, uint32_t num_buckets, uint32_t max_leaf, int 
         BV_TRY(hipMalloc(&d_bn, max_big * 3 * kMaxBuckets * sizeof(unsigned int)));
         BV_TRY(hipMalloc(&d_bb, max_big * 3 * kMaxBuckets * 6 * sizeof(unsigned long long)));
         phase("alloc");
-        BV_TRY(hipMemcpy(d_pb, boxes.data(), n * 6 * sizeof(double), hipMemcpyHostToDevice));
         hipLaunchKernelGGL(centroids, dim3(static_cast<uint32_t>((n + kThreads - 1) / kThreads)), dim3(kThreads), 0, 0,
                            d_pb, d_pc, n);
         hipLaunchKernelGGL(iota_order, dim3(static_cast<uint32_t>((n + kThreads - 1) / kThreads)), dim3(kThreads), 0, 0,
@@ -913,16 +910,16 @@ int device_build_bvh(crt_scene* s, uint32_t num_buckets, uint32_t max_leaf, int 
         }
         hipLaunchKernelGGL(emit_preorder, grid(0, nnodes), dim3(kThreads), 0, 0, d_nodes, d_pre, nnodes, d_out, d_maxleaf);
         BV_TRY(hipGetLastError());
-        s->nodes.resize(nnodes);
-        BV_TRY(hipMemcpy(s->nodes.data(), d_out, nnodes * sizeof(crt_bvh_node), hipMemcpyDeviceToHost));
-        BV_TRY(hipMemcpy(order.data(), d_order, n * 4, hipMemcpyDeviceToHost));
-        BV_TRY(hipMemcpy(&s->max_leaf, d_maxleaf, 4, hipMemcpyDeviceToHost));
-        s->depth = static_cast<uint32_t>(nl);
-        s->order = std::move(order);
+        BV_TRY(hipMemcpy(&out.max_leaf, d_maxleaf, 4, hipMemcpyDeviceToHost));
+        out.nnodes = nnodes;
+        out.depth = static_cast<uint32_t>(nl);
+        out.nodes = d_out;
+        out.order = d_order;
+        d_out = nullptr;
+        d_order = nullptr;
     }
-    phase("preorder + download");
+    phase("preorder");
 done:
-    (void)hipFree(d_pb);
     (void)hipFree(d_pc);
     (void)hipFree(d_order);
     (void)hipFree(d_f);
@@ -943,6 +940,38 @@ done:
     (void)hipFree(d_pre);
     (void)hipFree(d_maxleaf);
     (void)hipFree(d_out);
+    return rc;
+}
+
+// Builds s->nodes / s->order on `device` for the (non-empty, non-linear) primitive list, from the
+// primitives' boxes (6 doubles each, in primitive order, on the host).
+int device_build_bvh(crt_scene* s, uint32_t num_buckets, uint32_t max_leaf, int device,
+                     const BigVec<double>& boxes) {
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev)
+        return fail(CRT_E_NODEVICE, "GPU BVH build: device " + std::to_string(device) + " not visible");
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    (void)hipSetDevice(device);
+    const size_t n = s->prims.size();
+    int rc = CRT_OK;
+    double* d_pb = nullptr;
+    DeviceTree t;
+    {
+        BV_TRY(hipMalloc(&d_pb, n * 6 * sizeof(double)));
+        BV_TRY(hipMemcpy(d_pb, boxes.data(), n * 6 * sizeof(double), hipMemcpyHostToDevice));
+        rc = device_build_tree(n, d_pb, num_buckets, max_leaf, t);
+        if (rc) goto done;
+        s->nodes.resize(t.nnodes);
+        s->order.resize(n);
+        BV_TRY(hipMemcpy(s->nodes.data(), t.nodes, t.nnodes * sizeof(crt_bvh_node), hipMemcpyDeviceToHost));
+        BV_TRY(hipMemcpy(s->order.data(), t.order, n * 4, hipMemcpyDeviceToHost));
+        s->max_leaf = t.max_leaf;
+        s->depth = t.depth;
+    }
+done:
+    (void)hipFree(d_pb);
+    device_tree_free(t);
     (void)hipSetDevice(prev);
     return rc;
 }

@@ -2079,8 +2079,8 @@ static size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 // per element in parallel (parallel_for); the image is not zero-filled first, only the guard words
 // (and the padding, which nothing reads) are cleared.
 static void stage_image(crt_scene* s) {
-    const size_t n_nodes = s->dnodes.size(), n_refs = s->refs.size();
-    const size_t n_sp = s->spheres.size(), n_q = s->quads.size(), n_m = s->dmats.size();
+    const size_t n_nodes = s->num_dnodes, n_refs = s->num_prims;
+    const size_t n_sp = s->num_spheres, n_q = s->num_quads, n_m = s->num_dmats;
     size_t off[kArrCount + 1];
     const size_t total = device_layout(s, off);
     BigVec<char>& img = s->image;
@@ -2113,60 +2113,19 @@ static void stage_image(crt_scene* s) {
     std::atomic<bool> f32_bad{false};
     parallel_for(n_nodes, 4096, [&](size_t a, size_t b) {
         bool bad = false;
-        for (size_t i = a; i < b; ++i) {
-            const DevNode& n = s->dnodes[i];
-            DevNodeF& f = fnodes[i];
-            for (int k = 0; k < 6; ++k) {
-                f.b[k] = static_cast<float>(n.b[k]);  // round to nearest
-                if (!std::isinf(n.b[k]) && !(std::fabs(n.b[k]) <= kF32BoundMax)) bad = true;
-            }
-            if (n.count == 0 && n.index == n.flags + 1 && !(n.flags & 1u)) {
-                // interior: children side by side, the left one at an even index (stage()); the walk
-                // takes the right child as left | 32
-                f.w0 = n.axis;
-                f.w1 = n.flags << kNodeFShift;
-            } else if (n.count == 0) {
-                // the root of an empty tree (empty box, no children): an empty leaf
-                f.w0 = 0;
-                f.w1 = kLeafFlagF;
-            } else if (n.count == kSentinelCount) {
-                // "axis" 3: R.neg bit 3 (kZeroDir) is clear in the f32 walk, so the far child the
-                // walk stores at the sentinel (into the guard level) is w0 & ~31, the sentinel itself
-                f.w0 = (static_cast<uint32_t>(i) << kNodeFShift) | 3u;
-                f.w1 = kSentinelW1;
-            } else {
-                f.w0 = n.index;
-                f.w1 = kLeafFlagF | n.count;
-            }
-        }
+        for (size_t i = a; i < b; ++i) bad = node_record(s->dnodes[i], static_cast<uint32_t>(i), fnodes[i]) || bad;
         if (bad) f32_bad = true;
     });
     // sphere pair records of the f32 candidate filter (slots i, i + 1): half i of record i from
     // sphere i, the other half from sphere i + 1 (the last record's second half zero)
     DevSpherePair* spair = reinterpret_cast<DevSpherePair*>(at(kArrSpherePairs));
     std::atomic<bool> sph_bad{false};
-    auto pair_half = [&](size_t i, float& cx, float& cy, float& cz, float& r2e) {
-        const DevSphere& sp = s->spheres[i];
-        double dc2 = 0;
-        bool bad = false;
-        for (int k = 0; k < 3; ++k) {
-            if (!(std::fabs(sp.c[k]) <= kF32SphereMax)) bad = true;
-            const double e = sp.c[k] - static_cast<double>(static_cast<float>(sp.c[k]));
-            dc2 += e * e;
-        }
-        if (!(std::fabs(sp.r) <= kF32SphereMax)) bad = true;
-        cx = static_cast<float>(sp.c[0]);
-        cy = static_cast<float>(sp.c[1]);
-        cz = static_cast<float>(sp.c[2]);
-        r2e = static_cast<float>(sp.r * sp.r * (1 + 0x1p-14) + dc2 * 0x1p22);
-        return bad;
-    };
     parallel_for(n_sp, 4096, [&](size_t a, size_t b) {
         bool bad = false;
         for (size_t i = a; i < b; ++i) {
             DevSpherePair& r = spair[i];
-            bad = pair_half(i, r.cx[0], r.cy[0], r.cz[0], r.r2e[0]) || bad;
-            if (i + 1 < n_sp) (void)pair_half(i + 1, r.cx[1], r.cy[1], r.cz[1], r.r2e[1]);
+            bad = sphere_pair_half(s->spheres[i], r.cx[0], r.cy[0], r.cz[0], r.r2e[0]) || bad;
+            if (i + 1 < n_sp) (void)sphere_pair_half(s->spheres[i + 1], r.cx[1], r.cy[1], r.cz[1], r.r2e[1]);
             else r.cx[1] = r.cy[1] = r.cz[1] = r.r2e[1] = 0;
         }
         if (bad) sph_bad = true;
@@ -2180,68 +2139,23 @@ static void stage_image(crt_scene* s) {
         for (size_t i = a; i < b; ++i) {
             const DevQuad& q = s->quads[i];
             if (!quad_record(q.v, q.s1, q.s2, q.sn, quadf[i])) qb = true;
+            quadbox[i] = DevQuadBox{};  // a record quad_flat_box rejects stays zero
             if (!quad_flat_box(q.v, q.s1, q.s2, quadbox[i])) fb = true;
         }
         if (qb) quads_bad = true;
         if (fb) flat_bad = true;
     });
-    // Parallelogram-only scenes of axis-aligned parallelograms (slot = parallelogram): each
-    // leaf's flat boxes are grouped by the axis their box is flat on (x, then y, then z; slot
-    // order inside a group), each record keeps its slot's offset in the leaf (pad[0]) and the
-    // leaf's first record the group sizes (pad[1] = nx | ny << 8), so the filter runs one loop per
-    // axis with the flat axis' two slab values folded into one (leaf_step, flat_axis_candidate).
-    // The records' order only changes which iteration computes a candidate bit, not the bit.
-    // A record flat on no axis cannot occur here (quad_flat_box accepted every parallelogram, so
-    // each box is flat on one axis); should one appear, the scene leaves the flat-box filter
-    // rather than have flat_axis_candidate read a wrong axis.
+    // parallelogram-only scenes of axis-aligned parallelograms: each leaf's flat boxes grouped by
+    // their flat axis (regroup_leaf)
     std::atomic<bool> regroup_bad{false};
     if (!flat_bad && n_sp == 0 && n_q > 0) {
         parallel_for(n_nodes, 1 << 12, [&](size_t a, size_t b) {
-            DevQuadBox tmp[32];
-            for (size_t k = a; k < b; ++k) {
-                const DevNode& nd = s->dnodes[k];
-                if (nd.count == 0 || nd.count > 32 || nd.count == kSentinelCount) continue;
-                // the pad (node 1, crt_host.cpp): an empty-box leaf over slot 0 that no node
-                // refers to; regrouping it too would race with the real leaf of slot 0
-                if (k == 1 && !(nd.b[0] <= nd.b[1])) continue;
-                uint32_t n = 0, groups[3] = {0, 0, 0};
-                for (uint32_t axis = 0; axis < 3; ++axis)
-                    for (uint32_t j = 0; j < nd.count; ++j) {
-                        const DevQuadBox& r = quadbox[nd.index + j];
-                        uint32_t flat = 3;
-                        for (uint32_t q = 0; q < 3 && flat == 3; ++q)
-                            if (r.b[2 * q] == r.b[2 * q + 1]) flat = q;
-                        if (flat == 3) regroup_bad = true;
-                        if (flat == axis) {
-                            tmp[n] = r;
-                            tmp[n].pad[0] = j;
-                            ++n;
-                            ++groups[axis];
-                        }
-                    }
-                if (n != nd.count) continue;  // a record flat on no axis (regroup_bad)
-                tmp[0].pad[1] = groups[0] | groups[1] << 8;
-                std::memcpy(&quadbox[nd.index], tmp, nd.count * sizeof(DevQuadBox));
-            }
+            bool bad = false;
+            for (size_t k = a; k < b; ++k) bad = regroup_leaf(s->dnodes[k], k, quadbox) || bad;
+            if (bad) regroup_bad = true;
         });
     }
-    // Shading constants precomputed per slot, with the reference's own operations (IEEE f64, no
-    // contraction), so shade reads the values its divisions would give:
-    //   emit[0] of a non-emitting sphere slot = 1 / r (the normal's (p - c) / r, vec3d.h:34);
-    //   a Dielectric's colour (unused: attenuation 1) = the front-face ratio 1. / ri
-    //   (material.h:191) and reflectance's r0 (material.h:178-179) for the front and back ratio.
-    const auto shading_consts = [](DevMaterial& m, const DevSphere* sp) {
-        if (m.kind == CRT_DIELECTRIC) {
-            const auto r0 = [](double ratio) {
-                double r = (1 - ratio) / (1 + ratio);
-                return r * r;
-            };
-            m.color[0] = 1. / m.param;
-            m.color[1] = r0(1. / m.param);
-            m.color[2] = r0(m.param / 1.);
-        }
-        if (sp && m.kind != CRT_DIFFUSE_LIGHT) m.emit[0] = 1 / sp->r;
-    };
+    // shading constants per slot (shading_consts)
     DevMaterial* smrec = reinterpret_cast<DevMaterial*>(at(kArrSphereMrec));
     DevMaterial* qmrec = reinterpret_cast<DevMaterial*>(at(kArrQuadMrec));
     parallel_for(n_sp, 4096, [&](size_t a, size_t b) {
@@ -2263,32 +2177,12 @@ static void stage_image(crt_scene* s) {
     s->staged = true;
 }
 
-// Copy the scene into HBM of `device`: the staged image in one transfer. Uploads to different
-// devices run concurrently (render_multi uploads from one thread per device); the image is
-// staged once, under the scene's lock.
-int device_upload(crt_scene* s, int device) {
-    int rc = check_device(device);
-    if (rc) return rc;
-    std::lock_guard<std::mutex> lk(s->dev_mu[device]);
-    DeviceCopy& c = s->dev[device];
-    if (c.valid) return CRT_OK;
-    if (s->dnodes.size() >= (size_t{1} << (31 - kNodeFShift)))
-        return fail(CRT_E_INVALID, "BVH too large for the device node layout");
-    {
-        std::lock_guard<std::mutex> ls(s->mu);
-        if (!s->staged) stage_image(s);
-    }
+// The pointers of a scene copy at `base` (device_layout's arrays at their offsets).
+void device_bind_copy(crt_scene* s, int device, void* base, size_t total) {
     size_t off[kArrCount + 1];
-    const size_t total = device_layout(s, off);
-    DeviceGuard g(device);
-    void* base = nullptr;
-    HIP_TRY(hipMalloc(&base, total));
+    (void)device_layout(s, off);
+    DeviceCopy& c = s->dev[device];
     char* b = static_cast<char*>(base);
-    hipError_t e = hipMemcpy(b, s->image.data(), total, hipMemcpyHostToDevice);
-    if (e != hipSuccess) {
-        (void)hipFree(base);
-        return fail(CRT_E_HIP, std::string("scene upload: ") + hipGetErrorString(e));
-    }
     c.base = base;
     c.bytes = total;
     c.nodes = reinterpret_cast<DevNode*>(b + off[kArrNodes]);
@@ -2311,6 +2205,37 @@ int device_upload(crt_scene* s, int device) {
     c.quad_mrec = reinterpret_cast<DevMaterial*>(b + off[kArrQuadMrec]);
     c.guard = reinterpret_cast<unsigned long long*>(b + off[kArrGuard]);
     c.valid = true;
+}
+
+// Copy the scene into HBM of `device`: the staged image in one transfer. Uploads to different
+// devices run concurrently (render_multi uploads from one thread per device); the image is
+// staged once, under the scene's lock. A scene set up on a device (crt_stage_gpu.hip) is copied
+// from that device's HBM instead (its copy there is already in place).
+int device_upload(crt_scene* s, int device) {
+    int rc = check_device(device);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> lk(s->dev_mu[device]);
+    DeviceCopy& c = s->dev[device];
+    if (c.valid) return CRT_OK;
+    if (s->num_dnodes >= (size_t{1} << (31 - kNodeFShift)))
+        return fail(CRT_E_INVALID, "BVH too large for the device node layout");
+    if (s->image_device < 0) {
+        std::lock_guard<std::mutex> ls(s->mu);
+        if (!s->staged) stage_image(s);
+    }
+    size_t off[kArrCount + 1];
+    const size_t total = device_layout(s, off);
+    DeviceGuard g(device);
+    void* base = nullptr;
+    HIP_TRY(hipMalloc(&base, total));
+    hipError_t e = s->image_device >= 0
+                       ? hipMemcpyPeer(base, device, s->dev[s->image_device].base, s->image_device, total)
+                       : hipMemcpy(base, s->image.data(), total, hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        (void)hipFree(base);
+        return fail(CRT_E_HIP, std::string("scene upload: ") + hipGetErrorString(e));
+    }
+    device_bind_copy(s, device, base, total);
     return CRT_OK;
 }
 
@@ -2328,6 +2253,17 @@ int device_guard(crt_scene* s, int device, uint64_t* schlick_undecided, bool res
     HIP_TRY(hipMemcpy(&v, c.guard, sizeof v, hipMemcpyDeviceToHost));
     if (reset) HIP_TRY(hipMemset(c.guard, 0, sizeof v));
     *schlick_undecided = v;
+    return CRT_OK;
+}
+
+int device_image(crt_scene* s, int device, void* host, size_t bytes) {
+    int rc = device_upload(s, device);
+    if (rc) return rc;
+    const DeviceCopy& c = s->dev[device];
+    if (bytes != c.bytes)
+        return fail(CRT_E_INVALID, "crt_scene_image: bytes must be " + std::to_string(c.bytes));
+    DeviceGuard g(device);
+    HIP_TRY(hipMemcpy(host, c.base, c.bytes, hipMemcpyDeviceToHost));
     return CRT_OK;
 }
 
@@ -2590,19 +2526,19 @@ static int dispatch_render(const crt_scene* s, int device, const crt_camera* cam
                            double* d_rgb, hipStream_t st, crt_render_stats* count_stats) {
     // depth + 1 levels: walk_step stores the far child at level sp unconditionally
     const size_t stack_bytes = align16(static_cast<size_t>(s->depth + 1) * dev::kBlock * sizeof(SE));
-    W.bytes_nodes = static_cast<uint32_t>(align16(s->dnodes.size() * sizeof(DevNodeF)));
+    W.bytes_nodes = static_cast<uint32_t>(align16(s->num_dnodes * sizeof(DevNodeF)));
     // sphere-only scenes in f32 range stage the filter's pair records instead of refs + spheres
-    W.bytes_refs = W.spheres_f32 ? 0u : static_cast<uint32_t>(align16(s->refs.size() * 4));
-    W.bytes_spheres = static_cast<uint32_t>(align16(s->spheres.size() * (W.spheres_f32 ? sizeof(DevSpherePair)
+    W.bytes_refs = W.spheres_f32 ? 0u : static_cast<uint32_t>(align16(s->num_prims * 4));
+    W.bytes_spheres = static_cast<uint32_t>(align16(s->num_spheres * (W.spheres_f32 ? sizeof(DevSpherePair)
                                                                                          : sizeof(DevSphere))));
-    W.bytes_quads = static_cast<uint32_t>(align16(s->quads.size() * sizeof(DevQuad)));
-    W.bytes_quadf = W.quads_f32 ? static_cast<uint32_t>(s->quads.size() * (W.quads_flat ? sizeof(DevQuadBox) : sizeof(DevQuadF)))
+    W.bytes_quads = static_cast<uint32_t>(align16(s->num_quads * sizeof(DevQuad)));
+    W.bytes_quadf = W.quads_f32 ? static_cast<uint32_t>(s->num_quads * (W.quads_flat ? sizeof(DevQuadBox) : sizeof(DevQuadF)))
                                 : 0u;
     const size_t scene_bytes = static_cast<size_t>(W.bytes_nodes) + W.bytes_refs + W.bytes_spheres + W.bytes_quads +
                                W.bytes_quadf;
     const uint32_t level = static_cast<uint32_t>(dev::kBlock * sizeof(SE));  // one stack level
     // the sentinel is the last node; refs are byte offsets into the f32 node array
-    W.sentinel = static_cast<uint32_t>(s->dnodes.size() - 1) << kNodeFShift;
+    W.sentinel = static_cast<uint32_t>(s->num_dnodes - 1) << kNodeFShift;
     W.f32_ok = s->dev[device].f32_ok ? 1u : 0u;
     W.tmin32 = static_cast<float>(cam->t_min);
     const bool force_global = std::getenv("CRT_NO_LDS_SCENE") != nullptr;
@@ -2633,7 +2569,7 @@ static int dispatch_render(const crt_scene* s, int device, const crt_camera* cam
                         stack_at(scene_bytes) + stack_bytes + cam_bytes + (W.sphere_only ? kAccBytes : 0) +
                             (W.quads_flat ? kInvBytes : 0) <= budget5;
         const size_t budget = w5 ? budget5 : kLdsSceneBudget;
-        const uint32_t sph64 = static_cast<uint32_t>(s->spheres.size() * sizeof(DevSphere));
+        const uint32_t sph64 = static_cast<uint32_t>(s->num_spheres * sizeof(DevSphere));
         if (W.spheres_f32 && stack_at(scene_bytes + sph64) + stack_bytes + cam_bytes + (w5 ? kAccBytes : 0) <= budget)
             W.bytes_sph64 = sph64;
         W.lds_stack = stack_at(scene_bytes + W.bytes_sph64);
@@ -2651,7 +2587,7 @@ static int dispatch_render(const crt_scene* s, int device, const crt_camera* cam
     // limit); W.ntop counts bytes of f32 nodes
     const size_t per_block = 160 * 1024 * dev::kBlock / (256 * CRT_WAVES_PER_EU);  // LDS per block at the VGPR occupancy
     const bool no_top = std::getenv("CRT_NO_LDS_TOP") != nullptr;
-    const size_t all_nodes = s->dnodes.size() * sizeof(DevNodeF);
+    const size_t all_nodes = s->num_dnodes * sizeof(DevNodeF);
     auto top_bytes = [&](size_t room) {
         return no_top ? 0u : static_cast<uint32_t>(std::min(all_nodes, room / sizeof(DevNodeF) * sizeof(DevNodeF)));
     };
@@ -2709,9 +2645,9 @@ int device_render(const crt_scene* s, int device, const crt_camera* cam, const c
         }
         return CRT_OK;
     }
-    W.sphere_only = (s->quads.empty() && !s->spheres.empty()) ? 1u : 0u;
+    W.sphere_only = (s->num_quads == 0 && s->num_spheres != 0) ? 1u : 0u;
     W.spheres_f32 = (W.sphere_only && s->dev[device].spheres_f32_ok) ? 1u : 0u;
-    W.quads_f32 = (s->spheres.empty() && !s->quads.empty() && s->dev[device].quads_f32_ok) ? 1u : 0u;
+    W.quads_f32 = (s->num_spheres == 0 && s->num_quads != 0 && s->dev[device].quads_f32_ok) ? 1u : 0u;
     // the flat-box filter is the walk's f32 node test: it needs the walk's f32 range (f32_ok)
     W.quads_flat = (W.quads_f32 && s->dev[device].quads_flat_ok && s->dev[device].f32_ok) ? 1u : 0u;
     W.exact_slab = (s->exact_slab || std::getenv("CRT_EXACT_SLAB") != nullptr) ? 1u : 0u;
@@ -2720,7 +2656,7 @@ int device_render(const crt_scene* s, int device, const crt_camera* cam, const c
     hipStream_t st = static_cast<hipStream_t>(stream);
     if (count_stats) HIP_TRY(hipStreamCreate(&st));
     int r;
-    if ((s->dnodes.size() << kNodeFShift) <= 65536)  // every ref fits a u16 stack entry
+    if ((s->num_dnodes << kNodeFShift) <= 65536)  // every ref fits a u16 stack entry
         r = dispatch_render<uint16_t>(s, device, cam, W, d_rgb, st, count_stats);
     else
         r = dispatch_render<uint32_t>(s, device, cam, W, d_rgb, st, count_stats);
@@ -2738,10 +2674,17 @@ int device_closest_hits(crt_scene* s, int device, const double* rays, size_t n, 
     const DeviceCopy& c = s->dev[device];
     const uint32_t blocks = static_cast<uint32_t>((n + dev::kBlock - 1) / dev::kBlock);
     // ref -> primitive index: spheres at [0, nsp), parallelograms at [nsp, nsp + nq)
-    const size_t nsp = s->spheres.size(), nq = s->quads.size();
+    const size_t nsp = s->num_spheres, nq = s->num_quads;
     std::vector<uint32_t> ref_prim(std::max<size_t>(1, nsp + nq));
-    for (size_t slot = 0; slot < s->refs.size(); ++slot) {
-        uint32_t r = s->refs[slot];
+    std::vector<uint32_t> dev_refs;  // a scene set up on the device has no host refs
+    const uint32_t* refs = s->refs.data();
+    if (s->refs.size() != s->num_prims) {
+        dev_refs.resize(s->num_prims);
+        HIP_TRY(hipMemcpy(dev_refs.data(), c.refs, s->num_prims * 4, hipMemcpyDeviceToHost));
+        refs = dev_refs.data();
+    }
+    for (size_t slot = 0; slot < s->num_prims; ++slot) {
+        uint32_t r = refs[slot];
         ref_prim[(r & kRefQuad) ? nsp + (r & ~kRefQuad) : r] = s->order[slot];
     }
     double* d_rays = nullptr;

@@ -24,6 +24,7 @@
 #include <vector>
 
 #include "crt_internal.h"
+#include "crt_prims.h"
 
 namespace crt {
 
@@ -74,20 +75,9 @@ static inline V3 unit(V3 a) { return divv(a, mag(a)); }                         
 static inline V3 v3(const double* p) { return {p[0], p[1], p[2]}; }
 static inline void put(double* p, V3 a) { p[0] = a.x; p[1] = a.y; p[2] = a.z; }
 
-// std::fmin / std::fmax as the reference's g++ build evaluates them: calls into glibc, whose
-// x86-64 versions return the SECOND operand on a tie (so fmin(+0, -0) = -0) and the other operand
-// when one is NaN. clang inlines them with the operands commuted, which differs on signed zeros,
-// so the host code spells the glibc semantics out.
-static inline double gfmin(double x, double y) {
-    if (std::isnan(x)) return y;
-    if (std::isnan(y)) return x;
-    return x < y ? x : y;
-}
-static inline double gfmax(double x, double y) {
-    if (std::isnan(x)) return y;
-    if (std::isnan(y)) return x;
-    return x > y ? x : y;
-}
+// std::fmin / std::fmax with glibc's semantics (crt_prims.h)
+using prim::gfmax;
+using prim::gfmin;
 
 // ---- intervals / AABB (math/interval.h, acceleration/aabb.h) --------------------------------
 struct Iv {
@@ -120,97 +110,52 @@ static void box_put(double* b, const Box3& r) {
 // ---------------------------------------------------------------------------------------------
 // flattening: objects -> primitives (Scene::get_primitive_components, scene.h:85-106)
 
-static Prim make_sphere(V3 c, double r, uint32_t mat) {
-    Prim p{};
-    p.kind = CRT_SPHERE;
-    p.material = mat;
-    put(p.v, c);
-    p.v[3] = r;
-    // sphere.h:112-122: AABB::from_points({center - rv, center + rv})
-    V3 rv{r, r, r};
-    Box3 b;
-    b.merge(sub(c, rv));
-    b.merge(add(c, rv));
-    box_put(p.box, b);
-    return p;
-}
-
-static Prim make_quad(V3 v, V3 s1, V3 s2, uint32_t mat) {
-    Prim p{};
-    p.kind = CRT_PARALLELOGRAM;
-    p.material = mat;
-    // parallelogram.h:269-296
-    V3 n = cross(s1, s2);
-    V3 un = unit(n);
-    V3 sn = divv(n, mag2(n));
-    put(p.v + 0, v);
-    put(p.v + 3, s1);
-    put(p.v + 6, s2);
-    put(p.v + 9, un);
-    put(p.v + 12, sn);
-    Box3 b;
-    b.merge(v);
-    b.merge(add(v, s1));
-    b.merge(add(v, s2));
-    b.merge(add(add(v, s1), s2));
-    const double m = 1e-4;  // ensure_min_axis_length(1e-4), aabb.h:197-202
-    for (int i = 0; i < 3; ++i) {
-        if (b.a[i].size() < m) {
-            double pad = (m - b.a[i].size()) / 2;
-            b.a[i].min -= pad;
-            b.a[i].max += pad;
-        }
-    }
-    box_put(p.box, b);
-    return p;
-}
-
+// One object's primitives (crt_prims.h, shared with the device scene set-up)
 static void emit_object(const crt_object& o, Prim* out) {
-    switch (o.kind) {
-        case CRT_SPHERE:
-            out[0] = make_sphere(v3(o.v), o.v[3], o.material);
-            break;
-        case CRT_PARALLELOGRAM:
-            out[0] = make_quad(v3(o.v), v3(o.v + 3), v3(o.v + 6), o.material);
-            break;
-        default: {  // CRT_BOX, box.h:53-84: min/max corners, three sides, six faces in this order
-            double a0[3], a1[3];
-            for (int k = 0; k < 3; ++k) {
-                a0[k] = gfmin(o.v[k], o.v[3 + k]);   // box.h:64-65
-                a1[k] = gfmax(o.v[k], o.v[3 + k]);
-            }
-            const V3 mn = v3(a0), mx = v3(a1);
-            const V3 sx{mx.x - mn.x, 0, 0}, sy{0, mx.y - mn.y, 0}, sz{0, 0, mx.z - mn.z};
-            out[0] = make_quad(mn, sx, sy, o.material);
-            out[1] = make_quad(mn, sx, sz, o.material);
-            out[2] = make_quad(mn, sy, sz, o.material);
-            out[3] = make_quad(mx, neg(sx), neg(sy), o.material);
-            out[4] = make_quad(mx, neg(sx), neg(sz), o.material);
-            out[5] = make_quad(mx, neg(sy), neg(sz), o.material);
-            break;
-        }
+    const uint32_t np = prim::object_prims(o);
+    for (uint32_t j = 0; j < np; ++j) {
+        out[j].kind = prim::object_prim(o, j, out[j].v, out[j].box);
+        out[j].material = o.material;
     }
 }
 
-static int flatten(crt_scene* s, bool boxes) {
-    // validate in object order (first error wins), then emit in parallel at prefix offsets
-    const size_t no = s->objects.size();
-    std::vector<size_t> off(no + 1, 0);
+// The objects' and materials' validation, in object order (first error wins): the primitive
+// count, the sphere count and whether any object is a Box (six primitives).
+static int validate(const crt_material* materials, size_t nm, const crt_object* objects, size_t no,
+                    size_t* nprims, size_t* nspheres, bool* boxes) {
+    size_t np = 0, ns = 0;
+    bool bx = false;
     for (size_t i = 0; i < no; ++i) {
-        const crt_object& o = s->objects[i];
-        if (o.material >= s->materials.size())
+        const crt_object& o = objects[i];
+        if (o.material >= nm)
             return fail(CRT_E_INVALID, "object " + std::to_string(i) + " references material " +
                                            std::to_string(o.material) + " out of range");
         if (o.kind != CRT_SPHERE && o.kind != CRT_PARALLELOGRAM && o.kind != CRT_BOX)
             return fail(CRT_E_INVALID, "object " + std::to_string(i) + " has unknown kind " +
                                            std::to_string(o.kind));
-        off[i + 1] = off[i] + (o.kind == CRT_BOX ? 6 : 1);
+        np += o.kind == CRT_BOX ? 6 : 1;
+        ns += o.kind == CRT_SPHERE;
+        bx = bx || o.kind == CRT_BOX;
     }
-    for (size_t i = 0; i < s->materials.size(); ++i) {
-        uint32_t k = s->materials[i].kind;
+    for (size_t i = 0; i < nm; ++i) {
+        uint32_t k = materials[i].kind;
         if (k < CRT_LAMBERTIAN || k > CRT_DIFFUSE_LIGHT)
             return fail(CRT_E_INVALID, "material " + std::to_string(i) + " has unknown kind");
     }
+    *nprims = np;
+    *nspheres = ns;
+    *boxes = bx;
+    return CRT_OK;
+}
+
+static int flatten(crt_scene* s, bool boxes) {
+    // validate in object order (first error wins), then emit in parallel at prefix offsets
+    const size_t no = s->objects.size();
+    size_t np = 0, ns = 0;
+    bool bx = false;
+    if (int rc = validate(s->materials.data(), s->materials.size(), s->objects.data(), no, &np, &ns, &bx)) return rc;
+    std::vector<size_t> off(no + 1, 0);
+    for (size_t i = 0; i < no; ++i) off[i + 1] = off[i] + prim::object_prims(s->objects[i]);
     const auto tv = std::chrono::steady_clock::now();
     s->prims.resize(off[no]);
     // boxes: the GPU BVH build's input, written while the primitives are hot in cache
@@ -224,13 +169,15 @@ static int flatten(crt_scene* s, bool boxes) {
             if (boxes)
                 for (size_t j = off[i]; j < off[i + 1]; ++j, ++p) {
                     std::memcpy(&s->pbox[6 * j], p->box, 6 * sizeof(double));
-                    for (int k = 0; k < 6; ++k) nan = nan || std::isnan(p->box[k]);
+                    for (int k = 0; k < 6; ++k) nan = nan || !std::isfinite(p->box[k]);
                 }
         }
         if (nan) nan_box = true;
     });
-    // the GPU build reproduces the host fold only for NaN-free boxes (with a NaN, fmin/fmax pick
-    // by operand order in ways its order-preserving keys do not model): such scenes build on the host
+    // the GPU build reproduces the host build only for finite boxes (with a NaN, fmin/fmax pick by
+    // operand order in ways its order-preserving keys do not model; an infinite bound makes NaN
+    // centroids and areas, e.g. a sphere with a NaN centre folds to the empty box [inf, -inf]):
+    // such scenes build on the host
     if (nan_box) BigVec<double>().swap(s->pbox);
     if (std::getenv("CRT_DEBUG_BUILD"))
         std::fprintf(stderr, "flatten: emit %.3f ms\n", std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tv).count());
@@ -578,20 +525,13 @@ static void stage(crt_scene* s) {
     lap("slots");
     s->dmats.resize(s->materials.size());
     parallel_for(s->materials.size(), 1 << 14, [&](size_t a, size_t b) {
-        for (size_t i = a; i < b; ++i) {
-            const crt_material& m = s->materials[i];
-            DevMaterial& d = s->dmats[i];
-            d = DevMaterial{};
-            d.kind = m.kind;
-            d.color[0] = m.color[0]; d.color[1] = m.color[1]; d.color[2] = m.color[2];
-            d.param = m.param;
-            if (m.kind == CRT_DIFFUSE_LIGHT) {
-                // DiffuseLight::emit(): intensity * intrinsic_color -> each channel * intensity
-                for (int k = 0; k < 3; ++k) d.emit[k] = m.color[k] * m.param;
-            }
-        }
+        for (size_t i = a; i < b; ++i) s->dmats[i] = material_record(s->materials[i]);
     });
     lap("materials");
+    s->num_dnodes = s->dnodes.size();
+    s->num_spheres = s->spheres.size();
+    s->num_quads = s->quads.size();
+    s->num_dmats = s->dmats.size();
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1109,6 +1049,26 @@ int crt_scene_create(const crt_material* materials, size_t num_materials,
             std::fprintf(stderr, "scene phase %-8s %8.3f ms\n", what, std::chrono::duration<double, std::milli>(now - t0).count());
             t0 = now;
         };
+        // A GPU build sets the scene up on its device (crt_stage_gpu.hip): the objects and
+        // materials go straight to HBM and the device image is computed there (CRT_HOST_STAGE=1:
+        // the host path, which stages the same image on the host)
+        if (prm.build_device != 0 && prm.linear == 0 && num_objects != 0 && std::getenv("CRT_HOST_STAGE") == nullptr) {
+            size_t np = 0, ns = 0;
+            bool bx = false;
+            int rc = validate(materials, num_materials, objects, num_objects, &np, &ns, &bx);
+            if (rc) return rc;
+            if (np >= 0x7fffffffu) return fail(CRT_E_INVALID, "too many primitives");
+            lap("validate");
+            bool host_path = false;
+            rc = device_create_scene(s.get(), materials, num_materials, objects, num_objects, np, ns, bx, prm,
+                                     static_cast<int>(prm.build_device) - 1, &host_path);
+            if (rc) return rc;
+            lap("device");
+            if (!host_path) {
+                *out = s.release();
+                return CRT_OK;
+            }
+        }
         // copied in parallel chunks into huge-page backed arrays (millions: 2.1 M objects and materials)
         s->materials.resize(num_materials);
         s->objects.resize(num_objects);
@@ -1123,6 +1083,9 @@ int crt_scene_create(const crt_material* materials, size_t num_materials,
         if (rc) return rc;
         lap("flatten");
         if (s->prims.size() >= 0x7fffffffu) return fail(CRT_E_INVALID, "too many primitives");
+        s->num_objects = num_objects;
+        s->num_materials = num_materials;
+        s->num_prims = s->prims.size();
         s->linear = prm.linear != 0;
         rc = build_bvh(s.get(), prm);
         if (rc) return rc;
@@ -1140,11 +1103,11 @@ int crt_scene_info_get(const crt_scene* s, crt_scene_info* info) {
     clear_error();
     if (!s || !info) return fail(CRT_E_INVALID, "crt_scene_info_get: null argument");
     crt_scene_info r{};
-    r.num_objects = s->objects.size();
-    r.num_materials = s->materials.size();
-    r.num_primitives = s->prims.size();
-    r.num_spheres = s->spheres.size();
-    r.num_parallelograms = s->quads.size();
+    r.num_objects = s->num_objects;
+    r.num_materials = s->num_materials;
+    r.num_primitives = s->num_prims;
+    r.num_spheres = s->num_spheres;
+    r.num_parallelograms = s->num_quads;
     r.num_nodes = s->nodes.size();
     r.depth = s->depth;
     r.max_leaf_size = s->max_leaf;
@@ -1167,6 +1130,12 @@ int crt_scene_upload(crt_scene* s, int device) {
     clear_error();
     if (!s) return fail(CRT_E_INVALID, "crt_scene_upload: null scene");
     return device_upload(s, device);
+}
+
+int crt_scene_image(crt_scene* s, int device, void* host, size_t bytes) {
+    clear_error();
+    if (!s || !host) return fail(CRT_E_INVALID, "crt_scene_image: null argument");
+    return device_image(s, device, host, bytes);
 }
 
 void crt_scene_destroy(crt_scene* s) {

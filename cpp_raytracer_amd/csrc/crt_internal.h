@@ -146,6 +146,124 @@ struct alignas(16) DevMaterial {
 // kind's array. Spheres/quads are stored in slot order, so for a sphere-only scene ref == slot.
 constexpr uint32_t kRefQuad = 0x80000000u;
 
+// ---- the records of the device image, one definition for the host staging (crt_host.cpp
+// stage(), crt_device.hip stage_image) and the device scene set-up (crt_stage_gpu.hip) -------
+
+// A material as the render kernel reads it: DiffuseLight::emit() = intensity * colour
+// (material.h:261-263) precomputed, each channel * intensity.
+CRT_HD DevMaterial material_record(const crt_material& m) {
+    DevMaterial d{};
+    d.kind = m.kind;
+    d.color[0] = m.color[0];
+    d.color[1] = m.color[1];
+    d.color[2] = m.color[2];
+    d.param = m.param;
+    if (m.kind == CRT_DIFFUSE_LIGHT)
+        for (int k = 0; k < 3; ++k) d.emit[k] = m.color[k] * m.param;
+    return d;
+}
+
+// Shading constants of a per-slot material record, with the reference's own operations (IEEE
+// f64, no contraction), so shade reads the values its divisions would give:
+//   emit[0] of a non-emitting sphere slot = 1 / r (the normal's (p - c) / r, vec3d.h:34);
+//   a Dielectric's colour (unused: attenuation 1) = the front-face ratio 1. / ri
+//   (material.h:191) and reflectance's r0 (material.h:178-179) for the front and back ratio.
+CRT_HD void shading_consts(DevMaterial& m, const DevSphere* sp) {
+    if (m.kind == CRT_DIELECTRIC) {
+        double r = (1 - 1. / m.param) / (1 + 1. / m.param);
+        const double front = r * r;
+        r = (1 - m.param / 1.) / (1 + m.param / 1.);
+        m.color[0] = 1. / m.param;
+        m.color[1] = front;
+        m.color[2] = r * r;
+    }
+    if (sp && m.kind != CRT_DIFFUSE_LIGHT) m.emit[0] = 1 / sp->r;
+}
+
+// Half of a sphere pair record (DevSpherePair) from one sphere; true when the sphere is outside
+// the f32 filter's range.
+CRT_HD bool sphere_pair_half(const DevSphere& sp, float& cx, float& cy, float& cz, float& r2e) {
+    double dc2 = 0;
+    bool bad = false;
+    for (int k = 0; k < 3; ++k) {
+        if (!(std::fabs(sp.c[k]) <= kF32SphereMax)) bad = true;
+        const double e = sp.c[k] - static_cast<double>(static_cast<float>(sp.c[k]));
+        dc2 += e * e;
+    }
+    if (!(std::fabs(sp.r) <= kF32SphereMax)) bad = true;
+    cx = static_cast<float>(sp.c[0]);
+    cy = static_cast<float>(sp.c[1]);
+    cz = static_cast<float>(sp.c[2]);
+    r2e = static_cast<float>(sp.r * sp.r * (1 + 0x1p-14) + dc2 * 0x1p22);
+    return bad;
+}
+
+// The f32 walk record of device node i (DevNodeF); true when a finite bound is beyond the f32
+// walk's range.
+CRT_HD bool node_record(const DevNode& n, uint32_t i, DevNodeF& f) {
+    bool bad = false;
+    for (int k = 0; k < 6; ++k) {
+        f.b[k] = static_cast<float>(n.b[k]);  // round to nearest
+        if (!std::isinf(n.b[k]) && !(std::fabs(n.b[k]) <= kF32BoundMax)) bad = true;
+    }
+    if (n.count == 0 && n.index == n.flags + 1 && !(n.flags & 1u)) {
+        // interior: children side by side, the left one at an even index (stage()); the walk
+        // takes the right child as left | 32
+        f.w0 = n.axis;
+        f.w1 = n.flags << kNodeFShift;
+    } else if (n.count == 0) {
+        // the root of an empty tree (empty box, no children): an empty leaf
+        f.w0 = 0;
+        f.w1 = kLeafFlagF;
+    } else if (n.count == kSentinelCount) {
+        // "axis" 3: R.neg bit 3 (kZeroDir) is clear in the f32 walk, so the far child the
+        // walk stores at the sentinel (into the guard level) is w0 & ~31, the sentinel itself
+        f.w0 = (i << kNodeFShift) | 3u;
+        f.w1 = kSentinelW1;
+    } else {
+        f.w0 = n.index;
+        f.w1 = kLeafFlagF | n.count;
+    }
+    return bad;
+}
+
+// Parallelogram-only scenes of axis-aligned parallelograms (slot = parallelogram): the leaf's
+// flat boxes grouped by the axis their box is flat on (x, then y, then z; slot order inside a
+// group), each record keeping its slot's offset in the leaf (pad[0]) and the leaf's first record
+// the group sizes (pad[1] = nx | ny << 8), so the filter runs one loop per axis with the flat
+// axis' two slab values folded into one (leaf_step, flat_axis_candidate). The records' order only
+// changes which iteration computes a candidate bit, not the bit. A record flat on no axis cannot
+// occur (quad_flat_box accepted every parallelogram, so each box is flat on one axis); should one
+// appear, this returns true and the scene leaves the flat-box filter rather than have
+// flat_axis_candidate read a wrong axis. k = the node's device index.
+CRT_HD bool regroup_leaf(const DevNode& nd, size_t k, DevQuadBox* quadbox) {
+    if (nd.count == 0 || nd.count > 32 || nd.count == kSentinelCount) return false;
+    // the pad (node 1, crt_host.cpp stage()): an empty-box leaf over slot 0 that no node refers
+    // to; regrouping it too would race with the real leaf of slot 0
+    if (k == 1 && !(nd.b[0] <= nd.b[1])) return false;
+    DevQuadBox tmp[32];
+    uint32_t n = 0, groups[3] = {0, 0, 0};
+    bool bad = false;
+    for (uint32_t axis = 0; axis < 3; ++axis)
+        for (uint32_t j = 0; j < nd.count; ++j) {
+            const DevQuadBox& r = quadbox[nd.index + j];
+            uint32_t flat = 3;
+            for (uint32_t q = 0; q < 3 && flat == 3; ++q)
+                if (r.b[2 * q] == r.b[2 * q + 1]) flat = q;
+            if (flat == 3) bad = true;
+            if (flat == axis) {
+                tmp[n] = r;
+                tmp[n].pad[0] = j;
+                ++n;
+                ++groups[axis];
+            }
+        }
+    if (n != nd.count) return bad;
+    tmp[0].pad[1] = groups[0] | groups[1] << 8;
+    for (uint32_t j = 0; j < n; ++j) quadbox[nd.index + j] = tmp[j];
+    return bad;
+}
+
 struct DeviceCopy {
     bool valid = false;
     void* base = nullptr;
@@ -204,6 +322,13 @@ struct crt_scene {
     crt::BigVec<crt::DevQuad> quads;
     crt::BigVec<uint32_t> quad_mat;
     crt::BigVec<crt::DevMaterial> dmats;
+    // element counts of the device layout (device_layout), set by the host staging (stage()) or
+    // by the device scene set-up (crt_stage_gpu.hip), which leaves the host arrays above empty
+    size_t num_objects = 0, num_materials = 0, num_prims = 0;
+    size_t num_dnodes = 0, num_spheres = 0, num_quads = 0, num_dmats = 0;
+    // >= 0: the scene was staged on that device (its image is s->dev[image_device]'s allocation;
+    // other devices copy it from there); -1: staged on the host (s->image)
+    int image_device = -1;
     uint32_t depth = 0;
     uint32_t max_leaf = 0;
     double build_ms = 0;
@@ -225,11 +350,11 @@ enum DevArray { kArrNodes, kArrFNodes, kArrRefs, kArrSpheres, kArrSpherePairs, k
                 kArrQuadF, kArrQuadBox, kArrQuadMat, kArrMats, kArrSphereMrec, kArrQuadMrec, kArrGuard,
                 kArrCount };
 inline size_t device_layout(const crt_scene* s, size_t off[kArrCount + 1]) {
-    const size_t n_nodes = s->dnodes.size(), n_sp = s->spheres.size(), n_q = s->quads.size();
+    const size_t n_nodes = s->num_dnodes, n_sp = s->num_spheres, n_q = s->num_quads;
     const size_t bytes[kArrCount] = {
-        n_nodes * sizeof(DevNode), n_nodes * sizeof(DevNodeF), s->refs.size() * 4, n_sp * sizeof(DevSphere),
+        n_nodes * sizeof(DevNode), n_nodes * sizeof(DevNodeF), s->num_prims * 4, n_sp * sizeof(DevSphere),
         n_sp * sizeof(DevSpherePair), n_sp * 4, n_q * sizeof(DevQuad), n_q * sizeof(DevQuadF),
-        n_q * sizeof(DevQuadBox), n_q * 4, std::max<size_t>(1, s->dmats.size()) * sizeof(DevMaterial),
+        n_q * sizeof(DevQuadBox), n_q * 4, std::max<size_t>(1, s->num_dmats) * sizeof(DevMaterial),
         n_sp * sizeof(DevMaterial), n_q * sizeof(DevMaterial), 64};
     size_t o = 0;
     for (int i = 0; i < kArrCount; ++i) {
@@ -256,6 +381,23 @@ const char* device_build_info();
 int device_guard(crt_scene* s, int device, uint64_t* schlick_undecided, bool reset);
 int device_build_bvh(crt_scene* s, uint32_t num_buckets, uint32_t max_leaf, int device,
                      const BigVec<double>& boxes);
+void device_bind_copy(crt_scene* s, int device, void* base, size_t total);
+int device_image(crt_scene* s, int device, void* host, size_t bytes);
+// A tree built on the current device (crt_bvh_gpu.hip): the preorder node array (bvh.h:468-550)
+// and the slot order in HBM.
+struct DeviceTree {
+    crt_bvh_node* nodes = nullptr;
+    uint32_t* order = nullptr;   // slot -> primitive
+    uint32_t nnodes = 0, depth = 0, max_leaf = 0;
+};
+int device_build_tree(size_t n, const double* d_pb, uint32_t num_buckets, uint32_t max_leaf, DeviceTree& out);
+void device_tree_free(DeviceTree& t);
+// The scene set up on `device` from the caller's objects and materials (crt_stage_gpu.hip): the
+// primitives, the GPU BVH build and the device image, which becomes the scene's copy on that
+// device. *host_path = true (nothing done) when the scene must take the host path instead.
+int device_create_scene(crt_scene* s, const crt_material* materials, size_t num_materials,
+                        const crt_object* objects, size_t num_objects, size_t num_prims, size_t num_spheres,
+                        bool boxes, const crt_bvh_params& prm, int device, bool* host_path);
 int device_ppm_values(int device, const double* d_rgb, size_t n, int32_t* h_values, void* stream);
 // host: RGB::as_string's three integers for one pixel (std::pow, x86 int conversion)
 void ppm_pixel_host(const double rgb[3], int32_t out[3]);

@@ -101,7 +101,7 @@ CRT_HD void quad_ray32(const double o[3], const double d[3], double tmin, double
 
 // the filter record of a parallelogram (the ctor's v, s1, s2, sn in f64); false when it is outside
 // the filter's range (the scene then decides its parallelograms in f64)
-inline bool quad_record(const double v[3], const double s1[3], const double s2[3], const double sn[3],
+CRT_HD bool quad_record(const double v[3], const double s1[3], const double s2[3], const double sn[3],
                         DevQuadF& f) {
     double sn1 = 0, S1 = 0, S2 = 0;
     bool ok = true;
@@ -184,7 +184,7 @@ static_assert(sizeof(DevQuadBox) == 32, "flat quad box record");
 
 // the flat box of an axis-aligned parallelogram; false for any other one (or bounds beyond the
 // walk's 2^40 range)
-inline bool quad_flat_box(const double v[3], const double s1[3], const double s2[3], DevQuadBox& f) {
+CRT_HD bool quad_flat_box(const double v[3], const double s1[3], const double s2[3], DevQuadBox& f) {
     int a1 = -1, a2 = -1;
     for (int k = 0; k < 3; ++k) {
         if (s1[k] != 0) {

@@ -72,7 +72,9 @@ typedef struct crt_bvh_params {
     uint32_t num_buckets;
     uint32_t max_prims_in_node;
     uint32_t linear;
-    uint32_t build_device;  /* 0: build on the host; d + 1: build on GPU d (the same tree) */
+    uint32_t build_device;  /* 0: build on the host; d + 1: build on GPU d (the same tree), and
+                             * set the scene up on GPU d: its copy there is in place after
+                             * crt_scene_create (the same bytes the host staging uploads) */
 } crt_bvh_params;
 
 /* ---- camera ---------------------------------------------------------------------------- */
@@ -206,7 +208,8 @@ int crt_scene_build_named(const char* name, uint32_t seed, int has_seed,
                           crt_camera_settings* cam);
 
 /* Flatten (Scene::get_primitive_components, scene.h:85-106) and build the BVH (bvh.h:183-550)
- * on the host. params may be NULL (= {32, 12, 0}). */
+ * on the host, or with params->build_device on that GPU, where the whole scene is then set up.
+ * params may be NULL (= {32, 12, 0, 0}). */
 int crt_scene_create(const crt_material* materials, size_t num_materials,
                      const crt_object* objects, size_t num_objects,
                      const crt_bvh_params* params, crt_scene** out);
@@ -215,6 +218,9 @@ int crt_scene_info_get(const crt_scene* scene, crt_scene_info* info);
 int crt_scene_export_bvh(const crt_scene* scene, crt_bvh_node* nodes, uint32_t* prim_order);
 /* Copy the scene into HBM of `device` (synchronous). Idempotent. */
 int crt_scene_upload(crt_scene* scene, int device);
+/* The scene's copy in HBM of `device` (uploaded first if needed) copied to host memory: bytes =
+ * crt_scene_info.device_bytes. The layout is internal (tests and tooling compare copies). */
+int crt_scene_image(crt_scene* scene, int device, void* host, size_t bytes);
 void crt_scene_destroy(crt_scene* scene);
 
 /* Camera::init() (camera.h:87-157). */
