@@ -123,25 +123,51 @@ static void emit_object(const crt_object& o, Prim* out) {
 // count, the sphere count and whether any object is a Box (six primitives).
 static int validate(const crt_material* materials, size_t nm, const crt_object* objects, size_t no,
                     size_t* nprims, size_t* nspheres, bool* boxes) {
+    // in parallel chunks: each chunk's counts and its first bad object / material; the first bad
+    // one overall is reported (objects before materials), as a sequential pass would
+    constexpr size_t kChunk = 1 << 16;
+    const size_t nco = (no + kChunk - 1) / kChunk, ncm = (nm + kChunk - 1) / kChunk;
+    std::vector<size_t> cnp(nco, 0), cns(nco, 0), cbad(nco, SIZE_MAX), mbad(ncm, SIZE_MAX);
+    std::vector<char> cbx(nco, 0);
+    parallel_for(nco, 1, [&](size_t a, size_t b) {
+        for (size_t c = a; c < b; ++c)
+            for (size_t i = c * kChunk; i < std::min(no, (c + 1) * kChunk); ++i) {
+                const crt_object& o = objects[i];
+                if (o.material >= nm || (o.kind != CRT_SPHERE && o.kind != CRT_PARALLELOGRAM && o.kind != CRT_BOX)) {
+                    cbad[c] = i;
+                    break;
+                }
+                cnp[c] += o.kind == CRT_BOX ? 6 : 1;
+                cns[c] += o.kind == CRT_SPHERE;
+                cbx[c] |= o.kind == CRT_BOX;
+            }
+    });
+    parallel_for(ncm, 1, [&](size_t a, size_t b) {
+        for (size_t c = a; c < b; ++c)
+            for (size_t i = c * kChunk; i < std::min(nm, (c + 1) * kChunk); ++i)
+                if (materials[i].kind < CRT_LAMBERTIAN || materials[i].kind > CRT_DIFFUSE_LIGHT) {
+                    mbad[c] = i;
+                    break;
+                }
+    });
     size_t np = 0, ns = 0;
     bool bx = false;
-    for (size_t i = 0; i < no; ++i) {
-        const crt_object& o = objects[i];
-        if (o.material >= nm)
-            return fail(CRT_E_INVALID, "object " + std::to_string(i) + " references material " +
-                                           std::to_string(o.material) + " out of range");
-        if (o.kind != CRT_SPHERE && o.kind != CRT_PARALLELOGRAM && o.kind != CRT_BOX)
+    for (size_t c = 0; c < nco; ++c) {
+        if (cbad[c] != SIZE_MAX) {
+            const size_t i = cbad[c];
+            const crt_object& o = objects[i];
+            if (o.material >= nm)
+                return fail(CRT_E_INVALID, "object " + std::to_string(i) + " references material " +
+                                               std::to_string(o.material) + " out of range");
             return fail(CRT_E_INVALID, "object " + std::to_string(i) + " has unknown kind " +
                                            std::to_string(o.kind));
-        np += o.kind == CRT_BOX ? 6 : 1;
-        ns += o.kind == CRT_SPHERE;
-        bx = bx || o.kind == CRT_BOX;
+        }
+        np += cnp[c];
+        ns += cns[c];
+        bx = bx || cbx[c];
     }
-    for (size_t i = 0; i < nm; ++i) {
-        uint32_t k = materials[i].kind;
-        if (k < CRT_LAMBERTIAN || k > CRT_DIFFUSE_LIGHT)
-            return fail(CRT_E_INVALID, "material " + std::to_string(i) + " has unknown kind");
-    }
+    for (size_t c = 0; c < ncm; ++c)
+        if (mbad[c] != SIZE_MAX) return fail(CRT_E_INVALID, "material " + std::to_string(mbad[c]) + " has unknown kind");
     *nprims = np;
     *nspheres = ns;
     *boxes = bx;
