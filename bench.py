@@ -322,9 +322,11 @@ def main() -> int:
     data = crt.SceneData.named(args.scene, args.seed)
     data.camera = camera_with(data.camera, image_w=args.width, image_h=args.height,
                               samples_per_pixel=args.spp, max_depth=args.depth)
+    ts = time.perf_counter()
     scene = crt.GpuScene(data, build_device=local if len(data.objects) > 100000 else None)
     info = scene.info()
     scene.upload(local)
+    setup_ms = (time.perf_counter() - ts) * 1e3  # flattening, BVH build, staging, upload (untimed)
     cam = crt.resolve_camera(data.camera, args.base_seed)
     h, w = args.height, args.width
     rb = 4  # 4-row blocks: 800 rows deal exactly over 1, 2, 4, 8 ranks (16 left 7 vs 6 at N=8)
@@ -494,7 +496,7 @@ def main() -> int:
             "data": SCENE_DATA.get(args.scene, f"synthetic: {args.scene} scene of the reference's src/main.cpp"),
             "config": {"workload": workload,
                        "samples_per_step": h * w * args.spp, "primitives": int(info.num_primitives),
-                       "bvh_nodes": int(info.num_nodes), "partition": f"{rb}-row blocks over {world} ranks, "
+                       "bvh_nodes": int(info.num_nodes), "scene_setup_ms": round(setup_ms, 1), "partition": f"{rb}-row blocks over {world} ranks, "
                        "RCCL all-gather of tiles overlapped with the next frame" if distributed else "whole frame on one GPU",
                        "process_group": {"backend": dist.get_backend() if distributed else None,
                                          "world_size": dist.get_world_size() if distributed else 1,

@@ -261,7 +261,7 @@ __global__ __launch_bounds__(NT) void build_level(
     const Task* __restrict__ tasks, const double* __restrict__ pb, const double* __restrict__ pc,
     uint32_t* __restrict__ order, uint8_t* __restrict__ pred, uint32_t* __restrict__ scr_f,
     uint32_t* __restrict__ scr_t, TNode* __restrict__ nodes, uint32_t* __restrict__ node_ctr,
-    Task* __restrict__ next, uint32_t* __restrict__ next_ctr, Params P) {
+    Task* __restrict__ next, uint32_t* __restrict__ next_ctr, Params P, const uint32_t* __restrict__ task_count) {
     __shared__ double red[NT][6];
     __shared__ double cred[NT][6];
     __shared__ unsigned int bn[3][kMaxBuckets];
@@ -270,7 +270,12 @@ __global__ __launch_bounds__(NT) void build_level(
     __shared__ uint32_t wsum[NT / 64];
     __shared__ uint32_t s_ntrue;
 
-    const Task tk = tasks[blockIdx.x];
+    // one task per block, or (task_count given: levels launched without a host round trip) the
+    // level's tasks strided over a grid of resident blocks
+    const uint32_t ntasks = task_count ? *task_count : gridDim.x;
+    for (uint32_t ti = blockIdx.x; ti < ntasks; ti += gridDim.x) {
+    __syncthreads();  // the previous task's reads of the shared arrays are done
+    const Task tk = tasks[ti];
     const uint32_t lo = tk.lo, hi = tk.hi, count = hi - lo, t = threadIdx.x;
 
     // 1. bounds (ordered fold over contiguous chunks) and centroid bounds
@@ -284,7 +289,7 @@ __global__ __launch_bounds__(NT) void build_level(
             me->leaf = 1;
             me->axis = 0;
         }
-        return;
+        continue;
     }
 
     // 2. bucket counts and boxes per axis
@@ -333,7 +338,7 @@ __global__ __launch_bounds__(NT) void build_level(
             me->axis = 0;
         }
     }
-    if (!split) return;
+    if (!split) continue;
 
     // 4. std::partition (libstdc++ bidirectional): predicate, then pair the falses of the left
     //    part with the trues of the right part from the outside in
@@ -396,7 +401,11 @@ __global__ __launch_bounds__(NT) void build_level(
         next[q] = Task{lo, mid, c, 0};
         next[q + 1] = Task{mid, hi, c + 1, 0};
     }
+    }
 }
+
+// the node count after a level (its build ids end there)
+__global__ void mark_level(const uint32_t* __restrict__ node_ctr, uint32_t* __restrict__ out) { *out = *node_ctr; }
 
 
 // ---- tasks above kBigTask primitives: each level spreads them over chunks of kChunk -----------
@@ -784,7 +793,13 @@ int device_build_tree(size_t n, const double* d_pb, uint32_t num_buckets, uint32
     unsigned long long* d_bb = nullptr;
     uint32_t nnodes = 0;
     std::vector<uint32_t> level_end;  // build ids [level_end[L - 1], level_end[L]) are level L
-    uint32_t *d_size = nullptr, *d_pre = nullptr, *d_maxleaf = nullptr;
+    uint32_t *d_size = nullptr, *d_pre = nullptr, *d_maxleaf = nullptr, *d_batch = nullptr;
+    constexpr uint32_t kBatch = 8;
+    // CRT_BVH_BATCH_LEVELS=1: the small-task levels in batches without host round trips (below);
+    // default: one host round trip per level throughout (the round-4 loop)
+    const bool async_levels = std::getenv("CRT_BVH_BATCH_LEVELS") != nullptr;
+    int dev_id = 0;
+    (void)hipGetDevice(&dev_id);
     crt_bvh_node* d_out = nullptr;
     const bool dbg = std::getenv("CRT_DEBUG_BUILD") != nullptr;
     auto tp = std::chrono::steady_clock::now();
@@ -839,6 +854,7 @@ int device_build_tree(size_t n, const double* d_pb, uint32_t num_buckets, uint32
         int level = 0;
         std::vector<ChunkInfo> chunks;
         while (nsmall || nbig) {
+            if (!nbig && async_levels) break;  // only small tasks left: the batched loop below
             if (nbig) {
                 chunks.clear();
                 for (uint32_t i = 0; i < nbig; ++i) {
@@ -867,7 +883,7 @@ int device_build_tree(size_t n, const double* d_pb, uint32_t num_buckets, uint32
             }
             if (nsmall) {
                 hipLaunchKernelGGL(build_level<kSmallThreads>, dim3(nsmall), dim3(kSmallThreads), 0, 0, d_ta, d_pb, d_pc, d_order,
-                                   d_pred, d_f, d_t, d_nodes, d_ctr, d_tb, d_ctr + 1, P);
+                                   d_pred, d_f, d_t, d_nodes, d_ctr, d_tb, d_ctr + 1, P, nullptr);
                 BV_TRY(hipGetLastError());
             }
             BV_TRY(hipMemcpy(ctr, d_ctr, sizeof ctr, hipMemcpyDeviceToHost));
@@ -888,6 +904,40 @@ int device_build_tree(size_t n, const double* d_pb, uint32_t num_buckets, uint32
             ctr[1] = ctr[2] = 0;
             BV_TRY(hipMemcpy(d_ctr + 1, &ctr[1], 8, hipMemcpyHostToDevice));
             std::swap(d_ta, d_tb);
+        }
+        // Only tasks of at most kBigTask primitives left: kBatch levels at a time with no host round
+        // trip between them. Level j of a batch reads its task count from cnt[j] and appends the
+        // next level's tasks to cnt[j + 1] (zeroed with the batch), striding them over a grid of
+        // resident blocks; its node count goes to lend[j]; the host reads the batch's counters once.
+        if (nsmall) {
+            int cus = 0;
+            BV_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev_id));
+            const uint32_t resident = static_cast<uint32_t>(std::max(1, cus)) * 8;  // ~17.5 KB of LDS a block
+            BV_TRY(hipMalloc(&d_batch, (2 * kBatch + 1) * 4));
+            std::vector<uint32_t> hb(2 * kBatch + 1);
+            uint32_t count = nsmall;
+            while (count) {
+                std::fill(hb.begin(), hb.end(), 0u);
+                hb[0] = count;
+                BV_TRY(hipMemcpy(d_batch, hb.data(), hb.size() * 4, hipMemcpyHostToDevice));
+                for (uint32_t j = 0; j < kBatch; ++j) {
+                    const uint32_t g = j == 0 ? std::min(count, resident) : resident;
+                    hipLaunchKernelGGL(build_level<kSmallThreads>, dim3(g), dim3(kSmallThreads), 0, 0, d_ta, d_pb, d_pc,
+                                       d_order, d_pred, d_f, d_t, d_nodes, d_ctr, d_tb, d_batch + j + 1, P, d_batch + j);
+                    hipLaunchKernelGGL(mark_level, dim3(1), dim3(1), 0, 0, d_ctr, d_batch + kBatch + 1 + j);
+                    std::swap(d_ta, d_tb);
+                }
+                BV_TRY(hipGetLastError());
+                BV_TRY(hipMemcpy(hb.data(), d_batch, hb.size() * 4, hipMemcpyDeviceToHost));
+                for (uint32_t j = 0; j < kBatch; ++j) {
+                    if (dbg)
+                        std::fprintf(stderr, "bvh level %d: %u small tasks (batched)\n", level, hb[j]);
+                    ++level;
+                    if (hb[kBatch + 1 + j] > level_end.back()) level_end.push_back(hb[kBatch + 1 + j]);
+                }
+                count = hb[kBatch];
+            }
+            ctr[0] = level_end.back();
         }
         phase("levels");
         nnodes = ctr[0];
@@ -940,6 +990,7 @@ done:
     (void)hipFree(d_pre);
     (void)hipFree(d_maxleaf);
     (void)hipFree(d_out);
+    (void)hipFree(d_batch);
     return rc;
 }
 
