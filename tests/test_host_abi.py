@@ -129,6 +129,32 @@ def test_empty_scene_and_bad_inputs(crt):
         crt.GpuScene(bad)
 
 
+def test_first_bad_input_is_reported_across_chunks(crt):
+    """Validation runs in 65536-object chunks in parallel; the message still names the first bad
+    object in object order, objects before materials."""
+    d = crt.SceneData.named("millions", 42)
+    objs = d.objects.copy()
+    objs["kind"][200_001] = 9
+    objs["material"][70_000] = len(d.materials) + 5
+    objs["material"][150_000] = len(d.materials) + 6
+    d.objects = objs
+    with pytest.raises(crt.CrtError, match="^.*object 70000 references material"):
+        crt.GpuScene(d)
+    objs["material"][70_000] = 0
+    with pytest.raises(crt.CrtError, match="object 150000 references material"):
+        crt.GpuScene(d)
+    objs["material"][150_000] = 0
+    with pytest.raises(crt.CrtError, match="object 200001 has unknown kind 9"):
+        crt.GpuScene(d)
+    objs["kind"][200_001] = 1
+    mats = d.materials.copy()
+    mats["kind"][1_000_000] = 0
+    mats["kind"][900_000] = 8
+    d.materials = mats
+    with pytest.raises(crt.CrtError, match="material 900000 has unknown kind"):
+        crt.GpuScene(d)
+
+
 def test_box_expands_to_six_faces(crt):
     d = crt.SceneData.named("cornell")
     s = crt.GpuScene(d)
