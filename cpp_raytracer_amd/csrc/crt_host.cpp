@@ -121,34 +121,46 @@ static void emit_object(const crt_object& o, Prim* out) {
 
 // The objects' and materials' validation, in object order (first error wins): the primitive
 // count, the sphere count and whether any object is a Box (six primitives).
-static int validate(const crt_material* materials, size_t nm, const crt_object* objects, size_t no,
-                    size_t* nprims, size_t* nspheres, bool* boxes) {
+int validate_scene(const crt_material* materials, size_t nm, const crt_object* objects, size_t no,
+                   size_t* nprims, size_t* nspheres, bool* boxes) {
     // in parallel chunks: each chunk's counts and its first bad object / material; the first bad
     // one overall is reported (objects before materials), as a sequential pass would
     constexpr size_t kChunk = 1 << 16;
     const size_t nco = (no + kChunk - 1) / kChunk, ncm = (nm + kChunk - 1) / kChunk;
     std::vector<size_t> cnp(nco, 0), cns(nco, 0), cbad(nco, SIZE_MAX), mbad(ncm, SIZE_MAX);
     std::vector<char> cbx(nco, 0);
+    // (counts in locals, stored once per chunk: the per-chunk slots of neighbouring threads share
+    // cache lines)
     parallel_for(nco, 1, [&](size_t a, size_t b) {
-        for (size_t c = a; c < b; ++c)
+        for (size_t c = a; c < b; ++c) {
+            size_t np_c = 0, ns_c = 0, bad = SIZE_MAX;
+            bool bx_c = false;
             for (size_t i = c * kChunk; i < std::min(no, (c + 1) * kChunk); ++i) {
-                const crt_object& o = objects[i];
-                if (o.material >= nm || (o.kind != CRT_SPHERE && o.kind != CRT_PARALLELOGRAM && o.kind != CRT_BOX)) {
-                    cbad[c] = i;
+                const uint32_t kind = objects[i].kind, mat = objects[i].material;
+                if (mat >= nm || (kind != CRT_SPHERE && kind != CRT_PARALLELOGRAM && kind != CRT_BOX)) {
+                    bad = i;
                     break;
                 }
-                cnp[c] += o.kind == CRT_BOX ? 6 : 1;
-                cns[c] += o.kind == CRT_SPHERE;
-                cbx[c] |= o.kind == CRT_BOX;
+                np_c += kind == CRT_BOX ? 6 : 1;
+                ns_c += kind == CRT_SPHERE;
+                bx_c = bx_c || kind == CRT_BOX;
             }
+            cnp[c] = np_c;
+            cns[c] = ns_c;
+            cbx[c] = bx_c;
+            cbad[c] = bad;
+        }
     });
     parallel_for(ncm, 1, [&](size_t a, size_t b) {
-        for (size_t c = a; c < b; ++c)
+        for (size_t c = a; c < b; ++c) {
+            size_t bad = SIZE_MAX;
             for (size_t i = c * kChunk; i < std::min(nm, (c + 1) * kChunk); ++i)
                 if (materials[i].kind < CRT_LAMBERTIAN || materials[i].kind > CRT_DIFFUSE_LIGHT) {
-                    mbad[c] = i;
+                    bad = i;
                     break;
                 }
+            mbad[c] = bad;
+        }
     });
     size_t np = 0, ns = 0;
     bool bx = false;
@@ -179,7 +191,7 @@ static int flatten(crt_scene* s, bool boxes) {
     const size_t no = s->objects.size();
     size_t np = 0, ns = 0;
     bool bx = false;
-    if (int rc = validate(s->materials.data(), s->materials.size(), s->objects.data(), no, &np, &ns, &bx)) return rc;
+    if (int rc = validate_scene(s->materials.data(), s->materials.size(), s->objects.data(), no, &np, &ns, &bx)) return rc;
     std::vector<size_t> off(no + 1, 0);
     for (size_t i = 0; i < no; ++i) off[i + 1] = off[i] + prim::object_prims(s->objects[i]);
     const auto tv = std::chrono::steady_clock::now();
@@ -1079,15 +1091,9 @@ int crt_scene_create(const crt_material* materials, size_t num_materials,
         // materials go straight to HBM and the device image is computed there (CRT_HOST_STAGE=1:
         // the host path, which stages the same image on the host)
         if (prm.build_device != 0 && prm.linear == 0 && num_objects != 0 && std::getenv("CRT_HOST_STAGE") == nullptr) {
-            size_t np = 0, ns = 0;
-            bool bx = false;
-            int rc = validate(materials, num_materials, objects, num_objects, &np, &ns, &bx);
-            if (rc) return rc;
-            if (np >= 0x7fffffffu) return fail(CRT_E_INVALID, "too many primitives");
-            lap("validate");
             bool host_path = false;
-            rc = device_create_scene(s.get(), materials, num_materials, objects, num_objects, np, ns, bx, prm,
-                                     static_cast<int>(prm.build_device) - 1, &host_path);
+            int rc = device_create_scene(s.get(), materials, num_materials, objects, num_objects, prm,
+                                         static_cast<int>(prm.build_device) - 1, &host_path);
             if (rc) return rc;
             lap("device");
             if (!host_path) {

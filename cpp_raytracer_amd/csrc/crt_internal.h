@@ -396,8 +396,12 @@ void device_tree_free(DeviceTree& t);
 // primitives, the GPU BVH build and the device image, which becomes the scene's copy on that
 // device. *host_path = true (nothing done) when the scene must take the host path instead.
 int device_create_scene(crt_scene* s, const crt_material* materials, size_t num_materials,
-                        const crt_object* objects, size_t num_objects, size_t num_prims, size_t num_spheres,
-                        bool boxes, const crt_bvh_params& prm, int device, bool* host_path);
+                        const crt_object* objects, size_t num_objects, const crt_bvh_params& prm, int device,
+                        bool* host_path);
+// the host's validation of objects and materials (crt_host.cpp): CRT_OK or the error of the first
+// bad one, with the primitive / sphere counts and whether any object is a Box
+int validate_scene(const crt_material* materials, size_t nm, const crt_object* objects, size_t no,
+                   size_t* nprims, size_t* nspheres, bool* boxes);
 int device_ppm_values(int device, const double* d_rgb, size_t n, int32_t* h_values, void* stream);
 // host: RGB::as_string's three integers for one pixel (std::pow, x86 int conversion)
 void ppm_pixel_host(const double rgb[3], int32_t out[3]);

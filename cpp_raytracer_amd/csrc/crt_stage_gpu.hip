@@ -114,6 +114,42 @@ __global__ __launch_bounds__(kT) void scan_add(uint32_t* __restrict__ out, size_
     if (i < n) out[i] += tile_sum[i / kScanTile];
 }
 
+// ---- validation (crt_host.cpp validate_scene, on the device) ------------------------------------
+// stat[0] = first bad object, stat[1] = first bad material (~0u: none), stat[3] = spheres,
+// stat[4] = Boxes (sums over the objects, valid when no object is bad; stat[2] unused)
+__device__ __forceinline__ uint32_t block_sum(uint32_t v, uint32_t* lds) {
+    uint32_t total;
+    (void)block_exclusive_scan(v, lds, total);
+    return total;
+}
+
+__global__ __launch_bounds__(kT) void validate_objects(const crt_object* __restrict__ obj, size_t no, size_t nm,
+                                                       uint32_t* __restrict__ stat) {
+    __shared__ uint32_t lds[kT];
+    const size_t i = static_cast<size_t>(blockIdx.x) * kT + threadIdx.x;
+    uint32_t ns = 0, nb = 0;
+    if (i < no) {
+        const uint32_t kind = obj[i].kind, mat = obj[i].material;
+        if (mat >= nm || (kind != CRT_SPHERE && kind != CRT_PARALLELOGRAM && kind != CRT_BOX))
+            atomicMin(&stat[0], static_cast<uint32_t>(i));
+        ns = kind == CRT_SPHERE ? 1u : 0u;
+        nb = kind == CRT_BOX ? 1u : 0u;
+    }
+    ns = block_sum(ns, lds);
+    nb = block_sum(nb, lds);
+    if (threadIdx.x == 0) {
+        atomicAdd(&stat[3], ns);
+        atomicAdd(&stat[4], nb);
+    }
+}
+
+__global__ __launch_bounds__(kT) void validate_materials(const crt_material* __restrict__ mat, size_t nm,
+                                                         uint32_t* __restrict__ stat) {
+    const size_t i = static_cast<size_t>(blockIdx.x) * kT + threadIdx.x;
+    if (i < nm && (mat[i].kind < CRT_LAMBERTIAN || mat[i].kind > CRT_DIFFUSE_LIGHT))
+        atomicMin(&stat[1], static_cast<uint32_t>(i));
+}
+
 // ---- primitives ------------------------------------------------------------------------------
 __global__ __launch_bounds__(kT) void object_counts(const crt_object* __restrict__ obj, size_t no,
                                                     uint32_t* __restrict__ cnt) {
@@ -368,8 +404,8 @@ __global__ __launch_bounds__(kT) void regroup_leaves(const DevNode* __restrict__
     } while (0)
 
 int device_create_scene(crt_scene* s, const crt_material* materials, size_t num_materials,
-                        const crt_object* objects, size_t num_objects, size_t num_prims, size_t num_spheres,
-                        bool boxes, const crt_bvh_params& prm, int device, bool* host_path) {
+                        const crt_object* objects, size_t num_objects, const crt_bvh_params& prm, int device,
+                        bool* host_path) {
     using namespace stagegpu;
     *host_path = false;
     int ndev = 0;
@@ -387,8 +423,9 @@ int device_create_scene(crt_scene* s, const crt_material* materials, size_t num_
         std::fprintf(stderr, "device scene %-12s %8.3f ms\n", what, std::chrono::duration<double, std::milli>(now - tp).count());
         tp = now;
     };
-    const size_t n = num_prims, no = num_objects, nm = num_materials;
-    const size_t nq = n - num_spheres;
+    const size_t no = num_objects, nm = num_materials;
+    size_t n = 0, nq = 0, num_spheres = 0;
+    bool boxes = false;
     int rc = CRT_OK;
     crt_object* d_obj = nullptr;
     crt_material* d_mat = nullptr;
@@ -398,6 +435,7 @@ int device_create_scene(crt_scene* s, const crt_material* materials, size_t num_
     void* base = nullptr;
     DeviceTree t;
     uint32_t flags = 0;
+    uint32_t stat[5] = {~0u, ~0u, 0, 0, 0};
     std::vector<uint32_t> top;  // (node, position, child-base) triples
     size_t total = 0;
     // exclusive scan of in[0, m) into out[0, m]
@@ -408,15 +446,41 @@ int device_create_scene(crt_scene* s, const crt_material* materials, size_t num_
         hipLaunchKernelGGL(scan_add, grid_of(m), dim3(kT), 0, 0, out, m, d_tiles);
     };
     {
+        if (no >= 0x7fffffffu) {
+            rc = fail(CRT_E_INVALID, "too many primitives");
+            goto done;
+        }
         SG_TRY(hipMalloc(&d_obj, no * sizeof(crt_object)));
         SG_TRY(hipMalloc(&d_mat, std::max<size_t>(1, nm) * sizeof(crt_material)));
-        SG_TRY(hipMalloc(&d_flags, 4));
-        SG_TRY(hipMalloc(&d_tiles, (std::max(n, no) / kScanTile + 2) * 4));
-        SG_TRY(hipMalloc(&d_pb, n * 6 * sizeof(double)));
-        SG_TRY(hipMemset(d_flags, 0, 4));
+        SG_TRY(hipMalloc(&d_flags, 5 * 4));
+        SG_TRY(hipMemcpy(d_flags, stat, sizeof stat, hipMemcpyHostToDevice));
         SG_TRY(hipMemcpy(d_obj, objects, no * sizeof(crt_object), hipMemcpyHostToDevice));
         if (nm) SG_TRY(hipMemcpy(d_mat, materials, nm * sizeof(crt_material), hipMemcpyHostToDevice));
         phase("upload");
+        // validation on the device; the host's own pass words the error of a bad input
+        hipLaunchKernelGGL(validate_objects, grid_of(no), dim3(kT), 0, 0, d_obj, no, nm, d_flags);
+        if (nm) hipLaunchKernelGGL(validate_materials, grid_of(nm), dim3(kT), 0, 0, d_mat, nm, d_flags);
+        SG_TRY(hipGetLastError());
+        SG_TRY(hipMemcpy(stat, d_flags, sizeof stat, hipMemcpyDeviceToHost));
+        if (stat[0] != ~0u || stat[1] != ~0u) {
+            size_t np_h = 0, ns_h = 0;
+            bool bx_h = false;
+            rc = validate_scene(materials, nm, objects, no, &np_h, &ns_h, &bx_h);
+            if (rc == CRT_OK) rc = fail(CRT_E_INVALID, "device scene set-up: validation disagrees with the host's");
+            goto done;
+        }
+        n = no + 5 * static_cast<size_t>(stat[4]);  // a Box is six primitives
+        num_spheres = stat[3];
+        nq = n - num_spheres;
+        boxes = stat[4] != 0;
+        if (n >= 0x7fffffffu) {
+            rc = fail(CRT_E_INVALID, "too many primitives");
+            goto done;
+        }
+        SG_TRY(hipMemset(d_flags, 0, 4));
+        SG_TRY(hipMalloc(&d_tiles, (std::max(n, no) / kScanTile + 2) * 4));
+        SG_TRY(hipMalloc(&d_pb, n * 6 * sizeof(double)));
+        phase("validate");
         if (boxes) {  // primitive offsets per object and primitive -> object
             SG_TRY(hipMalloc(&d_cnt, no * 4));
             SG_TRY(hipMalloc(&d_off, (no + 1) * 4));

@@ -14,8 +14,8 @@ import cpp_raytracer_amd as crt  # noqa: E402
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 3
 d = crt.SceneData.named("millions", 42)
 crt.GpuScene(crt.SceneData.named("config1"), build_device=0).upload(0)  # warm up HIP
-for r in range(reps):
-    for route in ("device", "host"):
+for route in ("device", "host"):
+    for r in range(reps):
         if route == "host":
             os.environ["CRT_HOST_STAGE"] = "1"
         t0 = time.perf_counter()
