@@ -795,9 +795,6 @@ int device_build_tree(size_t n, const double* d_pb, uint32_t num_buckets, uint32
     std::vector<uint32_t> level_end;  // build ids [level_end[L - 1], level_end[L]) are level L
     uint32_t *d_size = nullptr, *d_pre = nullptr, *d_maxleaf = nullptr, *d_batch = nullptr;
     constexpr uint32_t kBatch = 8;
-    // CRT_BVH_BATCH_LEVELS=1: the small-task levels in batches without host round trips (below);
-    // default: one host round trip per level throughout (the round-4 loop)
-    const bool async_levels = std::getenv("CRT_BVH_BATCH_LEVELS") != nullptr;
     int dev_id = 0;
     (void)hipGetDevice(&dev_id);
     crt_bvh_node* d_out = nullptr;
@@ -854,7 +851,7 @@ int device_build_tree(size_t n, const double* d_pb, uint32_t num_buckets, uint32
         int level = 0;
         std::vector<ChunkInfo> chunks;
         while (nsmall || nbig) {
-            if (!nbig && async_levels) break;  // only small tasks left: the batched loop below
+            if (!nbig) break;  // only small tasks left: the batched loop below
             if (nbig) {
                 chunks.clear();
                 for (uint32_t i = 0; i < nbig; ++i) {
