@@ -17,8 +17,8 @@ mkdir -p "$OUT"
 import hashlib, subprocess, sys
 from bench import build_stamp
 st = build_stamp()
-srcs = ['csrc/crt_device.hip', 'csrc/crt_bvh_gpu.hip', 'csrc/crt_host.cpp', 'csrc/crt_internal.h',
-        'csrc/crt_quad_filter.h', '../include/crt_render.h', 'csrc/crt_schlick.h']
+srcs = subprocess.run(['make', '-s', '-C', 'cpp_raytracer_amd', 'stamp-srcs'], capture_output=True,
+                      text=True, check=True).stdout.split()
 h = hashlib.sha256(b''.join(open('cpp_raytracer_amd/' + f, 'rb').read() for f in srcs)).hexdigest()[:16]
 ok = not st['git_dirty'] and st['source_sha'] == h
 print(('pmc: library ' if ok else 'pmc: REFUSED, library ') + st['build_info'] + ' tree src=' + h)
