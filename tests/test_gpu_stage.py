@@ -118,3 +118,25 @@ def test_closest_hits_and_render_on_device_staged_scene(crt):
 @pytest.mark.slow
 def test_millions_device_image(crt):
     same_image(crt, crt.SceneData.named("millions", 42))
+
+
+@pytest.mark.slow
+def test_millions_with_boxes_and_parallelograms(crt):
+    """2.1 M spheres with Boxes and parallelograms mixed in: both device scans span many tiles
+    (over a thousand 2048-element tiles, so the tile sums are scanned in several chunks)."""
+    from cpp_raytracer_amd import OBJECT_DTYPE
+    rng = np.random.default_rng(3)
+    d = crt.SceneData.named("millions", 42)
+    n = 3000
+    extra = np.zeros(2 * n, OBJECT_DTYPE)
+    extra["kind"][:n] = 3
+    extra["kind"][n:] = 2
+    extra["material"] = rng.integers(0, len(d.materials), 2 * n)
+    a = rng.uniform(-300, 300, (2 * n, 3))
+    extra["v"][:n, :3] = a[:n]
+    extra["v"][:n, 3:6] = a[:n] + rng.uniform(0.2, 3, (n, 3))
+    extra["v"][n:, :3] = a[n:]
+    extra["v"][n:, 3:9] = rng.uniform(-2, 2, (n, 6))
+    objs = np.concatenate([d.objects, extra])
+    d.objects = objs[rng.permutation(len(objs))]
+    same_image(crt, d)
