@@ -512,6 +512,10 @@ int device_create_scene(crt_scene* s, const crt_material* materials, size_t num_
         phase("build");
         // the breadth-first top (stage()) and the child-bases of its unexpanded nodes
         const uint32_t nn = t.nnodes;
+        if (static_cast<size_t>(nn) + 2 >= (size_t{1} << (31 - kNodeFShift))) {  // device_upload's limit
+            rc = fail(CRT_E_INVALID, "BVH too large for the device node layout");
+            goto done;
+        }
         const auto& N = s->nodes;
         auto interior = [&](uint32_t i) { return N[i].count == 0 && i + 1 < nn; };
         std::vector<uint32_t> bfs{0};
