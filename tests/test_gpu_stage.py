@@ -140,3 +140,23 @@ def test_millions_with_boxes_and_parallelograms(crt):
     objs = np.concatenate([d.objects, extra])
     d.objects = objs[rng.permutation(len(objs))]
     same_image(crt, d)
+
+
+def test_device_set_up_frees_its_temporaries(crt):
+    """Creating and destroying a device-staged scene returns the device memory it took: the
+    temporaries of the set-up (objects, boxes, tree, scans) are freed at once, the copy at destroy."""
+    import torch
+    d = crt.SceneData.named("rtow_final", 42)
+    objs = np.concatenate([d.objects] * 400)  # 194k spheres: the device route
+    objs["v"][:, :3] += np.repeat(np.arange(400), len(d.objects))[:, None] * 30.0
+    d.objects = objs
+    crt.GpuScene(d, build_device=0).close()  # warm: runtime pools, module load
+    torch.cuda.synchronize()
+    free0, _ = torch.cuda.mem_get_info()
+    for _ in range(3):
+        g = crt.GpuScene(d, build_device=0)
+        assert g.info().device_bytes > 0
+        g.close()
+    torch.cuda.synchronize()
+    free1, _ = torch.cuda.mem_get_info()
+    assert free0 - free1 < 64 << 20, (free0, free1)
