@@ -267,6 +267,24 @@ def cpu_baseline(args, scene_data, log) -> dict | None:
     return None
 
 
+DIGESTS = ROOT / "tests" / "golden" / "frame_digests.json"
+
+
+def frame_check(workload: str, base_seed: int, digest: str, agree: bool, rank_digests: list, world: int) -> dict:
+    """The bench line's frame self-check: rank 0's frame digest, whether every rank assembled the
+    same frame, and whether it equals the N=1 digest recorded for this workload and base seed
+    (tests/golden/frame_digests.json, from a one-GPU run; null when none is recorded)."""
+    key = f"{workload}; base_seed {base_seed}"
+    try:
+        recorded = json.loads(DIGESTS.read_text()).get(key)
+    except (OSError, ValueError):
+        recorded = None
+    return {"frame_digest": digest, "ranks_agree": agree, "rank_digests": rank_digests if world > 1 else None,
+            "recorded_n1_digest": recorded, "matches_n1": (digest == recorded) if recorded else None,
+            "basis": "sha256 of the assembled float64 frame (first 15 hex digits), every rank; frames are "
+                     "bit-identical for any rank count"}
+
+
 def launch_check(args) -> int:
     """One rank of `--launch-check`: join the process group (gloo, CPU), agree on the world size
     with an all-reduce, rank 0 prints it."""
@@ -292,7 +310,7 @@ def main() -> int:
     import torch.distributed as dist
     import cpp_raytracer_amd as crt
     from cpp_raytracer_amd import Tiling, camera_with
-    from cpp_raytracer_amd.tiles import TileGather, owned_rows
+    from cpp_raytracer_amd.tiles import TileGather, digests_agree, frame_digest, owned_rows
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -392,6 +410,19 @@ def main() -> int:
     if args.dump_frame:  # every rank's last assembled frame (tests: equal to the 1-rank frame)
         import numpy as np
         np.save(f"{args.dump_frame}.rank{rank}.npy", assembled[0].cpu().numpy())
+    # self-check of the assembled frame (untimed): every rank hashes the frame it holds, the digests
+    # are all-gathered, and rank 0 compares them with each other and with the recorded N=1 digest
+    # of this workload (frames are bit-identical for any rank count). CRT_BENCH_CORRUPT_RANK=k
+    # (tests only) flips one value of rank k's frame first, which must flip ranks_agree.
+    final = assembled[0]
+    if os.environ.get("CRT_BENCH_CORRUPT_RANK", "") == str(rank):
+        final = final.clone()
+        final.view(-1)[final.numel() // 2] += 1.0
+    digest = frame_digest(final)
+    if distributed:
+        agree, rank_digests = digests_agree(digest, "cuda" if dist.get_backend() == "nccl" else "cpu")
+    else:
+        agree, rank_digests = True, [digest]
     if distributed:
         t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -467,6 +498,14 @@ def main() -> int:
                          "basis": "rocprofv3 PMC: 2 x FETCH_SIZE + WRITE_SIZE (MI355X_MICROARCH.md HBM section)"},
         },
     }
+    # the honest pair beside the issue-port figure: useful f64 work against the vector f64 peak,
+    # and issue-busy weighted by the share of lanes active per instruction
+    fp64_tflops = flops / (kernel_ms * 1e-3) / 1e12
+    roofline["useful_frac"] = round(fp64_tflops / FP64_VECTOR_PEAK_TFLOPS, 4)
+    roofline["useful_basis"] = ("algorithmic f64 flops (12 per node test, 23 per sphere test, 40 per "
+                                "parallelogram test, 50 per ray) / kernel time / 78.6 TF vector f64 peak")
+    roofline["lane_weighted_issue"] = (round(issue * pmc_data["valu_lane_utilization"], 4)
+                                       if issue is not None and "valu_lane_utilization" in pmc_data else None)
     if pmc_data is None:
         roofline["note"] = ("no PMC summary of this workload on this exact committed build (tools/gpu_pmc.sh): "
                             "issue fraction and traffic unmeasured")
@@ -530,6 +569,7 @@ def main() -> int:
                               "basis": "Dielectric draws a one-ulp different pow() could flip, counted by the "
                                        "kernel (crt_render_guard); 0 = frames bit-for-bit the reference's branches"},
             "cpu_baseline": cpu,
+            "frame_check": frame_check(workload, args.base_seed, digest, agree, rank_digests, world),
         }
         print(json.dumps(out), flush=True)
     if distributed:

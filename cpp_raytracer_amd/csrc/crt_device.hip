@@ -2231,6 +2231,10 @@ int device_upload(crt_scene* s, int device) {
     hipError_t e = s->image_device >= 0
                        ? hipMemcpyPeer(base, device, s->dev[s->image_device].base, s->image_device, total)
                        : hipMemcpy(base, s->image.data(), total, hipMemcpyHostToDevice);
+    // a peer copy also carries the source copy's guard words (its running Schlick count, counted
+    // into by renders on that device): a new copy starts at zero, as a host-staged one does
+    if (e == hipSuccess && s->image_device >= 0)
+        e = hipMemset(static_cast<char*>(base) + off[kArrGuard], 0, total - off[kArrGuard]);
     if (e != hipSuccess) {
         (void)hipFree(base);
         return fail(CRT_E_HIP, std::string("scene upload: ") + hipGetErrorString(e));

@@ -193,10 +193,11 @@ __global__ __launch_bounds__(kT) void scatter_top(const uint32_t* __restrict__ t
 
 // the device position of every preorder node (stage()'s breadth-first top, then sibling-pair
 // depth-first subtrees): from the root through the top to the node's frontier ancestor, then
-// down its depth-first expansion
+// down its depth-first expansion. A path of a well-formed tree has at most depth + 1 nodes, so
+// max_steps = the build's depth + 2 bounds both walks together; only a malformed tree exceeds it
 __global__ __launch_bounds__(kT) void node_positions(const crt_bvh_node* __restrict__ nd, uint32_t nn,
                                                      const uint32_t* __restrict__ tpos,
-                                                     const uint32_t* __restrict__ tbase,
+                                                     const uint32_t* __restrict__ tbase, uint32_t max_steps,
                                                      uint32_t* __restrict__ pos, uint32_t* __restrict__ flags) {
     const uint32_t i = blockIdx.x * kT + threadIdx.x;
     bool bad = false;
@@ -206,13 +207,13 @@ __global__ __launch_bounds__(kT) void node_positions(const crt_bvh_node* __restr
             uint32_t p = 0, steps = 0;
             for (;; ++steps) {  // the frontier ancestor: the last top node on the path
                 const uint32_t c = i < nd[p].index ? p + 1 : nd[p].index;
-                if (tpos[c] == kNone || steps > 4096) break;
+                if (tpos[c] == kNone || steps > max_steps) break;
                 p = c;
             }
             uint32_t base = tbase[p];  // breadth-first index of p's first child
             for (;; ++steps) {
                 const uint32_t l = p + 1, r = nd[p].index;
-                if (i == l || i == r || steps > 8192 || base == kNone || r <= l) {
+                if (i == l || i == r || steps > max_steps || base == kNone || r <= l) {
                     bad = !(i == l || i == r);
                     at = (i == r ? base + 1 : base) + 1;  // place(k) = k + 1 for k >= 1
                     break;
@@ -562,7 +563,8 @@ int device_create_scene(crt_scene* s, const crt_material* materials, size_t num_
         SG_TRY(hipMemcpy(d_top, top.data(), top.size() * 4, hipMemcpyHostToDevice));
         const uint32_t ntop = static_cast<uint32_t>(top.size() / 3);
         hipLaunchKernelGGL(scatter_top, grid_of(ntop), dim3(kT), 0, 0, d_top, ntop, d_tpos, d_tbase);
-        hipLaunchKernelGGL(node_positions, grid_of(nn), dim3(kT), 0, 0, t.nodes, nn, d_tpos, d_tbase, d_pos, d_flags);
+        hipLaunchKernelGGL(node_positions, grid_of(nn), dim3(kT), 0, 0, t.nodes, nn, d_tpos, d_tbase,
+                           static_cast<uint32_t>(t.depth) + 2u, d_pos, d_flags);
         auto* dn = reinterpret_cast<DevNode*>(b + off[kArrNodes]);
         hipLaunchKernelGGL(emit_nodes, grid_of(nn), dim3(kT), 0, 0, t.nodes, nn, d_pos, dn,
                            reinterpret_cast<DevNodeF*>(b + off[kArrFNodes]), d_flags);

@@ -68,3 +68,23 @@ class TileGather:
         out = torch.empty(self.h, self.w, 3, dtype=tile.dtype, device=tile.device)
         out.index_copy_(0, self.dst, self.full.index_select(0, self.src))
         return out
+
+
+def frame_digest(frame: torch.Tensor) -> str:
+    """sha256 of an assembled (h, w, 3) float64 frame's bytes, row-major (the Image layout,
+    image.h), as its first 15 hex digits (60 bits: one int64 over the wire). Frames are
+    bit-identical for any rank count, so this digest is too: an N-rank run must report the N=1
+    digest of the same workload."""
+    import hashlib
+    return hashlib.sha256(frame.detach().contiguous().cpu().numpy().tobytes()).hexdigest()[:15]
+
+
+def digests_agree(digest: str, device, group=None) -> tuple[bool, list[str]]:
+    """All-gather every rank's frame digest (one int64 per rank, on `device`: the process group's
+    device, cuda for RCCL); returns (all ranks equal, the digests in rank order)."""
+    world = dist.get_world_size(group)
+    mine = torch.tensor([int(digest, 16)], dtype=torch.int64, device=device)
+    every = torch.empty(world, dtype=torch.int64, device=device)
+    dist.all_gather_into_tensor(every, mine, group=group)
+    got = [f"{int(v):015x}" for v in every.cpu().tolist()]
+    return all(g == got[0] for g in got), got

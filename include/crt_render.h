@@ -25,7 +25,12 @@
 extern "C" {
 #endif
 
-#define CRT_ABI_VERSION 1
+/* ABI versions:
+ *   1  rounds 1-4.
+ *   2  round 5: crt_scene_image added; crt_bvh_params.build_device = d + 1 now also sets the scene
+ *      up on GPU d (its copy there lives as long as the scene; other devices peer-copy it, guard
+ *      words zeroed) and leaves the host-side staging image empty. */
+#define CRT_ABI_VERSION 2
 
 /* ---- status codes ---------------------------------------------------------------------- */
 #define CRT_OK 0

@@ -160,3 +160,23 @@ def test_device_set_up_frees_its_temporaries(crt):
     torch.cuda.synchronize()
     free1, _ = torch.cuda.mem_get_info()
     assert free0 - free1 < 64 << 20, (free0, free1)
+
+
+def test_peer_copy_to_second_device(crt):
+    """A device-staged scene reaches GPUs other than its build device by a peer copy of its HBM
+    image (device_upload). That copy must equal the host-staged image byte for byte — guard words
+    included: they start at zero, not at the source copy's running Schlick count — and a frame
+    rendered over two devices must equal the one-device frame. Needs two visible GPUs."""
+    import torch
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs two visible GPUs")
+    d = crt.SceneData.named("rtow_final", 42)
+    host = crt.GpuScene(d)
+    dev = crt.GpuScene(d, build_device=0)
+    cam = crt.resolve_camera(crt.camera_with(d.camera, image_w=64, image_h=40, samples_per_pixel=4,
+                                             max_depth=10), 7)
+    one = dev.render(cam)[0]  # counts into device 0's guard word before device 1 gets its copy
+    assert np.array_equal(host.device_image(1), dev.device_image(1))
+    two = dev.render(cam, num_devices=2)[0]
+    assert one.tobytes() == two.tobytes()
+    assert dev.guard(1) == 0

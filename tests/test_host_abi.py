@@ -24,7 +24,7 @@ def test_library_exports_every_declared_symbol(crt):
     assert len(names) >= 17
     for n in names:
         assert hasattr(lib, n), f"{n} declared in include/crt_render.h but not exported"
-    assert lib.crt_abi_version() == 1
+    assert lib.crt_abi_version() == 2
 
 
 def test_python_binding_covers_header(crt):
