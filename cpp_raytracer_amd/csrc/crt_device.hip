@@ -129,6 +129,7 @@ struct Work {
     // count per-round lane numbers (CRT_ROUND_COUNTERS=1; their atomics shift the phase timings)
     uint32_t count_spec, round_counters;
     uint32_t f32_ok;        // node bounds fit the f32 walk's error analysis (else f64 decides)
+    uint32_t pair_walk;     // HBM-scene kernels built with CRT_PAIR_WALK: walk_pairs for NaN-free rays
     uint32_t spheres_f32;   // sphere-only scene within the f32 filter's range (two-pass leaves)
     uint32_t quads_f32;     // parallelogram-only scene within its f32 filter's range (two-pass leaves)
     uint32_t quads_flat;    // ... and every parallelogram axis-aligned: pass 1 is the flat-box node test
@@ -1204,6 +1205,190 @@ __device__ __forceinline__ void walk(const SceneView& S, Stack<SE>& st, const do
     R.sp = static_cast<int32_t>(static_cast<uint32_t>(tp - empty)) / static_cast<int32_t>(st.stride);
 }
 
+// ---- the sibling-pair walk of the HBM-scene kernels (CRT_PAIR_WALK) ----------------------------
+// A step tests BOTH children of an entered interior node: one 64-byte read (siblings are side by
+// side, the left one 64-byte aligned, so a pair is one half of a 128-byte line) and two f32 node
+// tests. Deep trees in HBM walk a dependent chain of node reads; testing a pair per step halves
+// its length (config 4: ~38 node tests a ray, each an L1 / L2 latency).
+// The lane's position is a token: a pair's byte offset | kind, kind 0 / 1: both children (1: the
+// right one first), 2: the left child alone, 3: the right one alone. An entered interior child X
+// continues as token(X) = X.left | (the ray's sign on X's split axis); an entered leaf that cannot
+// be processed now (a far child) continues as its pair with kind 2 / 3, i.e. a re-test of its own
+// box.
+// Exactness (the primitive tests are the reference's, in its order, with its t_max):
+// - the DFS order of the children does not depend on t_max, and is the reference's
+//   (bvh.h:684-698: near child first by the sign of d on the parent's split axis);
+// - the node test is monotone in t_max and in the box: a child box lies inside its parent's
+//   (node boxes are unions of their primitives' boxes), and the rounded slab values satisfy
+//   near(child) >= near(parent), far(child) <= far(parent), so "child entered at t" implies
+//   "parent entered at t" and at any larger t_max;
+// - so testing a node at a t_max at least the reference's (children before their elder sibling's
+//   subtree has shrunk it) only adds node visits: a node the pair walk culls, the reference culls
+//   too, at its own (smaller or equal) t_max;
+// - and a leaf's primitives run only right after its box was entered at the current t_max: the
+//   first leaf a step enters (tested at the current t_max) exits to the leaf phase at once; every
+//   other leaf is re-tested (pair | bit) when the walk comes back to it. The reference tests a
+//   leaf's box iff every ancestor was entered at its (larger) t_max, which the entry of the leaf
+//   at the current t_max implies, so both test the same leaves at the same t_max.
+// - A popped interior token is not re-tested itself: its children are tested at the current
+//   t_max, and by monotonicity they all fail where the reference would cull it.
+// The speculative form (SPEC: Aila & Laine's postponed leaves, walk()): a lane that has recorded
+// its first leaf walks on with the t_max of now and parks at its second leaf as a re-test token,
+// so the leaf is tested again at the then-current t_max in the next round.
+// Stack: tokens, the far token stored at level sp unconditionally (pushed when both children are
+// entered and the near one is interior); the guard level holds the sentinel's token (sentinel
+// ref | 2: a pair whose right half, past the node array, is never tested). The root's token is
+// 0 | 2 (the pad node beside it is never tested). tests/test_pair_walk_model.py runs this state
+// machine against the reference's DFS on random trees.
+#ifndef CRT_PAIR_WALK
+#define CRT_PAIR_WALK 0
+#endif
+constexpr uint32_t kTokLeft = 2u, kTokMask = 63u;  // kTokLeft: the left child alone (root, sentinel)
+
+// v_cndmask_b32 with a lane mask from a ballot (scalar registers): m ? a : b per lane
+__device__ __forceinline__ uint32_t vsel(uint64_t m, uint32_t a, uint32_t b) {
+    uint32_t r;
+    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(b), "v"(a), "s"(m));
+    return r;
+}
+
+template <bool TOP>
+__device__ __forceinline__ void fetch_pair(const SceneView& S, uint32_t p, Uvec4& a0, Uvec4& a1, Uvec4& b0, Uvec4& b1) {
+    if (TOP) {
+        // the treelet is a whole number of pairs (dispatch_render), so a pair is in LDS or in HBM
+        const uint64_t hbm = __ballot(p >= S.ntop);
+        uint64_t save;
+        asm volatile(
+            "s_and_saveexec_b64 %[save], %[hbm]\n\t"
+            "s_cbranch_execz 1f\n\t"
+            "global_load_dwordx4 %[a0], %[p], %[base]\n\t"
+            "global_load_dwordx4 %[a1], %[p], %[base] offset:16\n\t"
+            "global_load_dwordx4 %[b0], %[p], %[base] offset:32\n\t"
+            "global_load_dwordx4 %[b1], %[p], %[base] offset:48\n"
+            "1:\n\t"
+            "s_andn2_b64 exec, %[save], %[hbm]\n\t"
+            "s_cbranch_execz 2f\n\t"
+            "ds_read_b128 %[a0], %[p]\n\t"
+            "ds_read_b128 %[a1], %[p] offset:16\n\t"
+            "ds_read_b128 %[b0], %[p] offset:32\n\t"
+            "ds_read_b128 %[b1], %[p] offset:48\n"
+            "2:\n\t"
+            "s_mov_b64 exec, %[save]\n\t"
+            "s_waitcnt vmcnt(0) lgkmcnt(0)"
+            : [a0] "=&v"(a0), [a1] "=&v"(a1), [b0] "=&v"(b0), [b1] "=&v"(b1), [save] "=&s"(save)
+            : [p] "v"(p), [hbm] "s"(hbm), [base] "s"(S.fnodes)
+            : "memory");
+    } else {
+        GlobalNodeF* q = (GlobalNodeF*)(reinterpret_cast<const char*>(S.fnodes) + p);
+        a0 = q[0].q0;
+        a1 = q[0].q1;
+        b0 = q[1].q0;
+        b1 = q[1].q1;
+    }
+}
+
+// the f32 node test of walk() on one child: gap' = hi' - lo' and its threshold
+__device__ __forceinline__ void child_gap(const Uvec4& q0, const Uvec4& q1, const Trav& R, float tmin32, float& gap,
+                                          float& th) {
+    const float x0 = __builtin_fmaf(__uint_as_float(q0.x), R.inv32[0], -R.oinv32[0]);
+    const float x1 = __builtin_fmaf(__uint_as_float(q0.y), R.inv32[0], -R.oinv32[0]);
+    const float y0 = __builtin_fmaf(__uint_as_float(q0.z), R.inv32[1], -R.oinv32[1]);
+    const float y1 = __builtin_fmaf(__uint_as_float(q0.w), R.inv32[1], -R.oinv32[1]);
+    const float z0 = __builtin_fmaf(__uint_as_float(q1.x), R.inv32[2], -R.oinv32[2]);
+    const float z1 = __builtin_fmaf(__uint_as_float(q1.y), R.inv32[2], -R.oinv32[2]);
+    const float lo = vmax3(vmin(x0, x1), vmin(y0, y1), vmax_s(vmin(z0, z1), tmin32));
+    const float hi = vmin3(vmax(x0, x1), vmax(y0, y1), vmin(vmax(z0, z1), R.tmax32));
+    gap = hi - lo;
+    th = __builtin_fmaf(vmax_abs(lo, hi), 0x1p-19f, R.marg);
+}
+
+template <typename SE, bool COUNT, bool TOP, bool INVL>
+__device__ __forceinline__ void walk_pairs(const SceneView& S, Stack<SE>& st, const double o[3], const double d[3],
+                                           double tmin, float tmin32, Trav& R, LaneCounters& ctr) {
+    const ptrdiff_t stride = static_cast<ptrdiff_t>(st.stride);
+    SE* const empty = st.base - stride;
+    SE* tp = st.base + (static_cast<ptrdiff_t>(R.sp) - 1) * stride;
+    uint32_t cur = R.cur;
+    uint32_t run = 1;
+    uint32_t pref = ~0u;  // the first leaf's re-test token (or the sentinel's), ~0u: none yet
+    // The per-lane logic is written on lane masks (uint64_t ballots: scalar ALU) with v_cndmask
+    // selects (vsel); as bools across the rare f64 branch, the compiler materialises the
+    // conditions as 0 / 1 in VGPRs and spends ~40 VALU a step on them.
+    uint64_t nop = __ballot(true);  // lanes with no leaf recorded yet
+    do {
+        CRT_WD(7, cur, static_cast<uint32_t>(tp - empty));
+        if (run) {
+            const uint32_t p = cur & ~kTokMask;
+            Uvec4 a0, a1, b0, b1;
+            fetch_pair<TOP>(S, p, a0, a1, b0, b1);
+            const uint32_t top = *tp;  // speculative pop
+            float gl, tl, gr, tr;
+            child_gap(a0, a1, R, tmin32, gl, tl);
+            child_gap(b0, b1, R, tmin32, gr, tr);
+            // token kind (cur & 3): 0 both children, near = left; 1 both, near = right; 2 the left
+            // child alone (a re-test); 3 the right child alone
+            const uint32_t kind = cur & 3u;
+            const uint64_t ml = __ballot(kind != 3u), mr = __ballot(kind != 2u), sw = __ballot(kind == 1u);
+            uint64_t el = __ballot(gl > 0.f) & ml, er = __ballot(gr > 0.f) & mr;
+            const uint64_t ul = ml & ~__ballot(fabsf(gl) > tl), ur = mr & ~__ballot(fabsf(gr) > tr);
+            if (COUNT) {
+                if (a1.w != kSentinelW1) ctr.nodes += kind != 3u ? 1 : 0;
+                ctr.nodes += kind != 2u ? 1 : 0;
+                if (wave_leader()) ctr.it_walk++;
+            }
+            if (__builtin_expect((ul | ur) != 0, 0)) {  // lanes the f32 margin cannot decide: f64
+                if (COUNT && wave_leader()) ctr.it_slow++;
+                const uint64_t me = 1ull << (threadIdx.x & 63);
+                bool fl = false, fr = false;
+                if (ul & me) {
+                    if (COUNT) ctr.slow_nodes++;
+                    fl = INVL ? slab64_inv(node64(S, p), o, S.inv64_lds, tmin, R.tmax) : slab64(node64(S, p), o, d, tmin, R.tmax);
+                }
+                if (ur & me) {
+                    if (COUNT) ctr.slow_nodes++;
+                    fr = INVL ? slab64_inv(node64(S, p + 32), o, S.inv64_lds, tmin, R.tmax)
+                              : slab64(node64(S, p + 32), o, d, tmin, R.tmax);
+                }
+                el = (el & ~ul) | __ballot(fl);
+                er = (er & ~ur) | __ballot(fr);
+            }
+            const uint64_t il = __ballot(a1.w < kLeafFlagF), ir = __ballot(b1.w < kLeafFlagF);
+            const uint64_t sent = __ballot(a1.w == kSentinelW1);  // the sentinel is a left child
+            // X: the first entered child in the reference's order (the right one first when sw)
+            const uint64_t xr = er & (sw | ~el);
+            const uint64_t both = el & er, any = el | er;
+            const uint64_t xi = (xr & ir) | (~xr & il);
+            // an entered leaf: the first one is recorded and the walk goes on with its
+            // continuation (the far token, or the stack top); the second one, and the sentinel,
+            // park as their re-test token (the far token pushed when both were entered)
+            const uint64_t leaf = any & ~xi;
+            const uint64_t park = leaf & (~nop | (~xr & sent));
+            const uint64_t dp = (any & xi) | park;  // cur = X's token
+            // the children's tokens: an interior child's own pair in the ray's order, a leaf's
+            // re-test (kind 2 / 3)
+            const uint32_t tokl = vsel(il, __builtin_amdgcn_ubfe(R.neg, a1.z, 1) | a1.w, p | 2u);
+            const uint32_t tokr = vsel(ir, __builtin_amdgcn_ubfe(R.neg, b1.z, 1) | b1.w, p | 3u);
+            const uint32_t tf = vsel(sw, tokl, tokr);  // the far child (pushed when both entered)
+            const uint32_t tx = vsel(xr, tokr, tokl);
+            pref = vsel(leaf & nop, tx, pref);
+            tp[stride] = static_cast<SE>(tf);
+            cur = vsel(dp, tx, vsel(both, tf, top));
+            tp += (static_cast<int32_t>(vsel(dp, 0u, ~0u)) + static_cast<int32_t>(vsel(both, 1u, 0u))) * stride;
+            run = vsel(park, 0u, 1u);
+        }
+        nop = __ballot(pref == ~0u);
+    } while (nop != 0);
+    {
+        // the recorded leaf's node: a re-test token's pair, + 32 for the right child (kind 3)
+        const Uvec2 w = fetch_nodef_words<TOP, false>(S, (pref & ~kTokMask) | ((pref & 1u) << 5));
+        R.state = w.y == kSentinelW1 ? kDone : kLeaf;
+        R.first = w.x;
+        R.count = w.y & ~kLeafFlagF;
+    }
+    R.cur = cur;
+    R.sp = static_cast<int32_t>(static_cast<uint32_t>(tp - empty)) / static_cast<int32_t>(st.stride);
+}
+
 // the entered leaf's primitives in order (bvh.h:635-652), then "return" to the DFS.
 // Sphere-only scenes store spheres in slot order, so the slot indexes them directly and the next
 // sphere is loaded while the current one is tested.
@@ -1690,6 +1875,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W5 ? kMa
     // the five-wave flat-parallelogram instance keeps each ray's f64 1 / d in LDS for the walk's f64
     // node tests (slab64_inv) instead of dividing at each one
     constexpr bool kInvLds = (kFlatOnly && LSCENE && W5) || (!LSCENE && !GSTACK);
+    // the sibling-pair walk (walk_pairs) of the HBM-scene instances; the instrumented pass walks
+    // that way only when it walks like the timed kernel (CRT_COUNT_SPEC=1)
+    constexpr bool kPair = CRT_PAIR_WALK && !LSCENE;
+    const bool pw = kPair && W.pair_walk && (!COUNT || W.count_spec);
     S.inv64_lds = W.lds_inv64;
     if (kAccLds) {
         acc_l[0] = 0;
@@ -1790,8 +1979,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W5 ? kMa
         // the guard level below the stack gets the sentinel back (the f32 walk's store at the
         // sentinel overwrote it)
         if (start || cont) {
-            st.base[-static_cast<ptrdiff_t>(st.stride)] = static_cast<SE>(W.sentinel);
             trav_init(P.o, P.d, W.f32_ok != 0, R);
+            // the pair walk's lanes hold tokens (walk_pairs): the root pair's left child, and the
+            // sentinel's token in the guard level; rays that need the EXACT walk keep plain refs
+            const bool tok = kPair && pw && !(R.neg & kZeroDir);
+            st.base[-static_cast<ptrdiff_t>(st.stride)] = static_cast<SE>(W.sentinel | (tok ? kTokLeft : 0u));
+            if (tok) R.cur = kTokLeft;
             if (kInvLds) {  // the f64 node test's 1 / d, divided once per ray (slab64_inv)
                 uint32_t t = threadIdx.x;
                 asm volatile("" : "+v"(t));
@@ -1818,7 +2011,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W5 ? kMa
             }
             if (COUNT) cw -= static_cast<uint32_t>(wall_clock64());
             set_prio<kPrioWalk>();
-            if (!W.exact_slab && __ballot(R.state == kWalk && (R.neg & kZeroDir)) == 0) {
+            if (kPair && pw) {
+                // W.pair_walk is off for scenes that need the EXACT walk (W.exact_slab); a ray
+                // with a zero / tiny / huge direction component takes it, on plain refs
+                if (__ballot(R.state == kWalk && (R.neg & kZeroDir)) != 0) {
+                    if (R.state == kWalk && (R.neg & kZeroDir))
+                        walk<SE, COUNT, true, kTopTreelet && !LSCENE, LSCENE, GSTACK, false>(S, st, P.o, P.d, C.t_min, tmin32, R, ctr);
+                }
+                if (R.state == kWalk && !(R.neg & kZeroDir))
+                    walk_pairs<SE, COUNT, kTopTreelet && !LSCENE, kInvLds>(S, st, P.o, P.d, C.t_min, tmin32, R, ctr);
+            } else if (!W.exact_slab && __ballot(R.state == kWalk && (R.neg & kZeroDir)) == 0) {
                 if (R.state == kWalk) {
                     if (!COUNT || W.count_spec)
                         walk<SE, COUNT, false, kTopTreelet && !LSCENE, LSCENE, GSTACK, true, kInvLds>(S, st, P.o, P.d, C.t_min, tmin32, R, ctr);
@@ -2593,7 +2795,8 @@ static int dispatch_render(const crt_scene* s, int device, const crt_camera* cam
     const bool no_top = std::getenv("CRT_NO_LDS_TOP") != nullptr;
     const size_t all_nodes = s->num_dnodes * sizeof(DevNodeF);
     auto top_bytes = [&](size_t room) {
-        return no_top ? 0u : static_cast<uint32_t>(std::min(all_nodes, room / sizeof(DevNodeF) * sizeof(DevNodeF)));
+        // whole 64-byte sibling pairs (walk_pairs reads a pair from LDS or from HBM, not both)
+        return no_top ? 0u : static_cast<uint32_t>(std::min(all_nodes, room / (2 * sizeof(DevNodeF)) * (2 * sizeof(DevNodeF))));
     };
     if (stack_bytes <= kLdsStackBudget && std::getenv("CRT_FORCE_GSTACK") == nullptr) {
         const size_t taken = stack_bytes + 2 * level + kInvBytes;
@@ -2655,6 +2858,7 @@ int device_render(const crt_scene* s, int device, const crt_camera* cam, const c
     // the flat-box filter is the walk's f32 node test: it needs the walk's f32 range (f32_ok)
     W.quads_flat = (W.quads_f32 && s->dev[device].quads_flat_ok && s->dev[device].f32_ok) ? 1u : 0u;
     W.exact_slab = (s->exact_slab || std::getenv("CRT_EXACT_SLAB") != nullptr) ? 1u : 0u;
+    W.pair_walk = (CRT_PAIR_WALK && !W.exact_slab && std::getenv("CRT_NO_PAIR_WALK") == nullptr) ? 1u : 0u;
     W.count_spec = std::getenv("CRT_COUNT_SPEC") != nullptr ? 1u : 0u;
     W.round_counters = std::getenv("CRT_ROUND_COUNTERS") != nullptr ? 1u : 0u;
     hipStream_t st = static_cast<hipStream_t>(stream);
@@ -3033,7 +3237,7 @@ const char* device_build_info() {
     return "arch=" CRT_ARCH " CRT_BLOCK=" CRT_STR(CRT_BLOCK) " CRT_TILE_W=" CRT_STR(CRT_TILE_W)
            " CRT_WAVES_PER_EU=" CRT_STR(CRT_WAVES_PER_EU) " CRT_WAVES_PER_EU_LDS=" CRT_STR(CRT_WAVES_PER_EU_LDS)
            " CRT_SHADE_BATCH=" CRT_STR(CRT_SHADE_BATCH) " CRT_CHUNK_MIN=" CRT_STR(CRT_CHUNK_MIN)
-           " CRT_WATCHDOG=" CRT_STR(CRT_WATCHDOG);
+           " CRT_WATCHDOG=" CRT_STR(CRT_WATCHDOG) " CRT_PAIR_WALK=" CRT_STR(CRT_PAIR_WALK);
 }
 
 }  // namespace crt
