@@ -565,6 +565,10 @@ def main() -> int:
                                 "candidate_wave_iters_per_filter_wave_iter": round(cnt.wave_iters_candidates / max(1, cnt.wave_iters_leaf), 4)},
             "f32_walk": {"f64_decided_node_tests": round(cnt.slow_node_tests / max(1, cnt.nodes_visited), 6),
                          "walk_iters_with_f64": round(cnt.wave_iters_slow / max(1, cnt.wave_iters_walk), 6)},
+            # raw counts of both instrumented passes (wave iterations per phase, lanes' tests):
+            # the basis of DESIGN §5's per-phase VALU attribution (tools/valu_attribution.py)
+            "instrumented_counts": {name: {f: int(getattr(c, f)) for f, _ in c._fields_ if f != "kernel_ms"}
+                                    for name, c in (("timed_walk", cnt_spec), ("plain_walk", cnt))},
             "schlick_guard": {"undecided_draws": guard, "frames": args.warmup + args.steps + 2,
                               "basis": "Dielectric draws a one-ulp different pow() could flip, counted by the "
                                        "kernel (crt_render_guard); 0 = frames bit-for-bit the reference's branches"},
