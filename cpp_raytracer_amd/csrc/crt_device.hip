@@ -416,6 +416,11 @@ __device__ __forceinline__ float vmax3_0(float a, float b) {  // max(a, b, 0)
     asm("v_max3_f32 %0, %1, %2, 0" : "=v"(r) : "v"(a), "v"(b));
     return r;
 }
+__device__ __forceinline__ float vmed3(float a, float b, float c) {
+    float r;
+    asm("v_med3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
 __device__ __forceinline__ float vmax3(float a, float b, float c) {
     float r;
     asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
@@ -864,7 +869,12 @@ __device__ __forceinline__ void trav_init(const double o[3], const double d[3], 
 //   gap' >  th  =>  gap > 0: far > near, near < tmax, far > tmin  (enter)
 //   gap' < -th  =>  gap < 0: far < near, far < tmin or tmax < near (no entry)
 // and only lanes with |gap'| <= th (grazing rays, ties, rays with marg = inf) run the f64 test on
-// the f64 node. Every decision is the f64 test's, so each ray visits the reference's node
+// the f64 node.
+// hi' takes med3(z0', z1', tmax') for min(max(z0', z1'), tmax') (one instruction fewer a node,
+// round 6): they differ only when tmax' < min(z0', z1'), and then lo' >= min(z0', z1') >= hi', so
+// gap' <= 0 is never "enter"; a "miss" has gap'(std) <= gap' < -th, and th is no smaller than the
+// standard one (hi' >= hi'(std) > 0 where they differ, else hi' equals it), so the standard
+// bound still proves it. Every decision is the f64 test's, so each ray visits the reference's node
 // sequence. The f32 test is 18 single-rate instructions where the f64 one is 25 half-rate ones.
 typedef __attribute__((address_space(3))) const unsigned char LdsByte;
 struct NodeLines {
@@ -1142,7 +1152,7 @@ __device__ __forceinline__ void walk(const SceneView& S, Stack<SE>& st, const do
                 const float z0 = __builtin_fmaf(__uint_as_float(q1.x), R.inv32[2], -R.oinv32[2]);
                 const float z1 = __builtin_fmaf(__uint_as_float(q1.y), R.inv32[2], -R.oinv32[2]);
                 const float lo = vmax3(vmin(x0, x1), vmin(y0, y1), vmax_s(vmin(z0, z1), tmin32));
-                const float hi = vmin3(vmax(x0, x1), vmax(y0, y1), vmin(vmax(z0, z1), R.tmax32));
+                const float hi = vmin3(vmax(x0, x1), vmax(y0, y1), vmed3(z0, z1, R.tmax32));
                 const float gap = hi - lo;
                 const float th = __builtin_fmaf(vmax_abs(lo, hi), 0x1p-19f, R.marg);
                 bool enter = gap > 0.f;
@@ -1212,7 +1222,7 @@ __device__ __forceinline__ void walk(const SceneView& S, Stack<SE>& st, const do
             const float z0 = __builtin_fmaf(__uint_as_float(q1.x), R.inv32[2], -R.oinv32[2]);
             const float z1 = __builtin_fmaf(__uint_as_float(q1.y), R.inv32[2], -R.oinv32[2]);
             const float lo = vmax3(vmin(x0, x1), vmin(y0, y1), vmax_s(vmin(z0, z1), tmin32));
-            const float hi = vmin3(vmax(x0, x1), vmax(y0, y1), vmin(vmax(z0, z1), R.tmax32));
+            const float hi = vmin3(vmax(x0, x1), vmax(y0, y1), vmed3(z0, z1, R.tmax32));
             const float gap = hi - lo;
             const float th = __builtin_fmaf(vmax_abs(lo, hi), 0x1p-19f, R.marg);
             bool enter = gap > 0.f;
@@ -1257,11 +1267,12 @@ __device__ __forceinline__ void walk(const SceneView& S, Stack<SE>& st, const do
 // side, the left one 64-byte aligned, so a pair is one half of a 128-byte line) and two f32 node
 // tests. Deep trees in HBM walk a dependent chain of node reads; testing a pair per step halves
 // its length (config 4: ~38 node tests a ray, each an L1 / L2 latency).
-// The lane's position is a token: a pair's byte offset | kind, kind 0 / 1: both children (1: the
-// right one first), 2: the left child alone, 3: the right one alone. An entered interior child X
-// continues as token(X) = X.left | (the ray's sign on X's split axis); an entered leaf that cannot
-// be processed now (a far child) continues as its pair with kind 2 / 3, i.e. a re-test of its own
-// box.
+// The lane's position is a token: the byte offset of the first node to test, | 1 when it is to be
+// tested alone. Without the bit the step tests that node and its sibling (offset ^ 32: siblings
+// are side by side, 64-byte aligned), the first one being the near child of their parent in the
+// ray's order. An entered interior child X continues as token(X) = X.left | (the ray's sign on
+// X's split axis) << 5 = X's near child (the old walk's `near`); an entered leaf that cannot be
+// processed now (a far child) continues as its own offset | 1, i.e. a re-test of its box alone.
 // Exactness (the primitive tests are the reference's, in its order, with its t_max):
 // - the DFS order of the children does not depend on t_max, and is the reference's
 //   (bvh.h:684-698: near child first by the sign of d on the parent's split axis);
@@ -1274,7 +1285,7 @@ __device__ __forceinline__ void walk(const SceneView& S, Stack<SE>& st, const do
 //   too, at its own (smaller or equal) t_max;
 // - and a leaf's primitives run only right after its box was entered at the current t_max: the
 //   first leaf a step enters (tested at the current t_max) exits to the leaf phase at once; every
-//   other leaf is re-tested (pair | bit) when the walk comes back to it. The reference tests a
+//   other leaf is re-tested (its offset | 1) when the walk comes back to it. The reference tests a
 //   leaf's box iff every ancestor was entered at its (larger) t_max, which the entry of the leaf
 //   at the current t_max implies, so both test the same leaves at the same t_max.
 // - A popped interior token is not re-tested itself: its children are tested at the current
@@ -1283,17 +1294,17 @@ __device__ __forceinline__ void walk(const SceneView& S, Stack<SE>& st, const do
 // its first leaf walks on with the t_max of now and parks at its second leaf as a re-test token,
 // so the leaf is tested again at the then-current t_max in the next round.
 // Stack: tokens, the far token stored at level sp unconditionally (pushed when both children are
-// entered and the near one is interior); the guard level holds the sentinel's token (sentinel
-// ref | 2: a pair whose right half, past the node array, is never tested). The root's token is
-// 0 | 2 (the pad node beside it is never tested). tests/test_pair_walk_model.py runs this state
-// machine against the reference's DFS on random trees.
+// entered and the near one is interior); the guard level holds the sentinel's token (its offset
+// | 1: its "sibling", past the node array, is never tested). The root's token is 0 | 1 (the pad
+// node beside it is never tested). tests/test_pair_walk_model.py runs this state machine against
+// the reference's DFS on random trees.
 #ifndef CRT_PAIR_WALK
 #define CRT_PAIR_WALK 0
 #endif
 #ifndef CRT_FLAT_DECIDE
 #define CRT_FLAT_DECIDE 0
 #endif
-constexpr uint32_t kTokLeft = 2u, kTokMask = 63u;  // kTokLeft: the left child alone (root, sentinel)
+constexpr uint32_t kTokAlone = 1u;  // token bit 0: the first node alone (root, sentinel, re-tests)
 
 // v_cndmask_b32 with a lane mask from a ballot (scalar registers): m ? a : b per lane
 __device__ __forceinline__ uint32_t vsel(uint64_t m, uint32_t a, uint32_t b) {
@@ -1302,38 +1313,42 @@ __device__ __forceinline__ uint32_t vsel(uint64_t m, uint32_t a, uint32_t b) {
     return r;
 }
 
+// The step's two f32 nodes: f (the first) and g = f ^ 32, read from the LDS treelet or from HBM
+// (the treelet holds whole sibling pairs, dispatch_render, so f and g are on the same side),
+// both sides in flight together as in fetch_nodef.
 template <bool TOP>
-__device__ __forceinline__ void fetch_pair(const SceneView& S, uint32_t p, Uvec4& a0, Uvec4& a1, Uvec4& b0, Uvec4& b1) {
+__device__ __forceinline__ void fetch_two(const SceneView& S, uint32_t f, uint32_t g, Uvec4& a0, Uvec4& a1, Uvec4& b0,
+                                          Uvec4& b1) {
     if (TOP) {
-        // the treelet is a whole number of pairs (dispatch_render), so a pair is in LDS or in HBM
-        const uint64_t hbm = __ballot(p >= S.ntop);
+        const uint64_t hbm = __ballot(f >= S.ntop);
         uint64_t save;
         asm volatile(
             "s_and_saveexec_b64 %[save], %[hbm]\n\t"
             "s_cbranch_execz 1f\n\t"
-            "global_load_dwordx4 %[a0], %[p], %[base]\n\t"
-            "global_load_dwordx4 %[a1], %[p], %[base] offset:16\n\t"
-            "global_load_dwordx4 %[b0], %[p], %[base] offset:32\n\t"
-            "global_load_dwordx4 %[b1], %[p], %[base] offset:48\n"
+            "global_load_dwordx4 %[a0], %[f], %[base]\n\t"
+            "global_load_dwordx4 %[a1], %[f], %[base] offset:16\n\t"
+            "global_load_dwordx4 %[b0], %[g], %[base]\n\t"
+            "global_load_dwordx4 %[b1], %[g], %[base] offset:16\n"
             "1:\n\t"
             "s_andn2_b64 exec, %[save], %[hbm]\n\t"
             "s_cbranch_execz 2f\n\t"
-            "ds_read_b128 %[a0], %[p]\n\t"
-            "ds_read_b128 %[a1], %[p] offset:16\n\t"
-            "ds_read_b128 %[b0], %[p] offset:32\n\t"
-            "ds_read_b128 %[b1], %[p] offset:48\n"
+            "ds_read_b128 %[a0], %[f]\n\t"
+            "ds_read_b128 %[a1], %[f] offset:16\n\t"
+            "ds_read_b128 %[b0], %[g]\n\t"
+            "ds_read_b128 %[b1], %[g] offset:16\n"
             "2:\n\t"
             "s_mov_b64 exec, %[save]\n\t"
             "s_waitcnt vmcnt(0) lgkmcnt(0)"
             : [a0] "=&v"(a0), [a1] "=&v"(a1), [b0] "=&v"(b0), [b1] "=&v"(b1), [save] "=&s"(save)
-            : [p] "v"(p), [hbm] "s"(hbm), [base] "s"(S.fnodes)
+            : [f] "v"(f), [g] "v"(g), [hbm] "s"(hbm), [base] "s"(S.fnodes)
             : "memory");
     } else {
-        GlobalNodeF* q = (GlobalNodeF*)(reinterpret_cast<const char*>(S.fnodes) + p);
-        a0 = q[0].q0;
-        a1 = q[0].q1;
-        b0 = q[1].q0;
-        b1 = q[1].q1;
+        GlobalNodeF* qa = (GlobalNodeF*)(reinterpret_cast<const char*>(S.fnodes) + f);
+        GlobalNodeF* qb = (GlobalNodeF*)(reinterpret_cast<const char*>(S.fnodes) + g);
+        a0 = qa->q0;
+        a1 = qa->q1;
+        b0 = qb->q0;
+        b1 = qb->q1;
     }
 }
 
@@ -1347,7 +1362,7 @@ __device__ __forceinline__ void child_gap(const Uvec4& q0, const Uvec4& q1, cons
     const float z0 = __builtin_fmaf(__uint_as_float(q1.x), R.inv32[2], -R.oinv32[2]);
     const float z1 = __builtin_fmaf(__uint_as_float(q1.y), R.inv32[2], -R.oinv32[2]);
     const float lo = vmax3(vmin(x0, x1), vmin(y0, y1), vmax_s(vmin(z0, z1), tmin32));
-    const float hi = vmin3(vmax(x0, x1), vmax(y0, y1), vmin(vmax(z0, z1), R.tmax32));
+    const float hi = vmin3(vmax(x0, x1), vmax(y0, y1), vmed3(z0, z1, R.tmax32));
     gap = hi - lo;
     th = __builtin_fmaf(vmax_abs(lo, hi), 0x1p-19f, R.marg);
 }
@@ -1368,69 +1383,62 @@ __device__ __forceinline__ void walk_pairs(const SceneView& S, Stack<SE>& st, co
     do {
         CRT_WD(7, cur, static_cast<uint32_t>(tp - empty));
         if (run) {
-            const uint32_t p = cur & ~kTokMask;
+            const uint32_t f = cur & ~kTokAlone, g = f ^ 32u;  // the first node and its sibling
             Uvec4 a0, a1, b0, b1;
-            fetch_pair<TOP>(S, p, a0, a1, b0, b1);
+            fetch_two<TOP>(S, f, g, a0, a1, b0, b1);
             const uint32_t top = *tp;  // speculative pop
-            float gl, tl, gr, tr;
-            child_gap(a0, a1, R, tmin32, gl, tl);
-            child_gap(b0, b1, R, tmin32, gr, tr);
-            // token kind (cur & 3): 0 both children, near = left; 1 both, near = right; 2 the left
-            // child alone (a re-test); 3 the right child alone
-            const uint32_t kind = cur & 3u;
-            const uint64_t ml = __ballot(kind != 3u), mr = __ballot(kind != 2u), sw = __ballot(kind == 1u);
-            uint64_t el = __ballot(gl > 0.f) & ml, er = __ballot(gr > 0.f) & mr;
-            const uint64_t ul = ml & ~__ballot(fabsf(gl) > tl), ur = mr & ~__ballot(fabsf(gr) > tr);
+            float g1, t1, g2, t2;
+            child_gap(a0, a1, R, tmin32, g1, t1);
+            child_gap(b0, b1, R, tmin32, g2, t2);
+            const uint64_t two = __ballot(cur == f);  // the sibling is tested too
+            uint64_t e1 = __ballot(g1 > 0.f), e2 = __ballot(g2 > 0.f) & two;
+            const uint64_t u1 = __ballot(!(fabsf(g1) > t1)), u2 = two & __ballot(!(fabsf(g2) > t2));
             if (COUNT) {
-                if (a1.w != kSentinelW1) ctr.nodes += kind != 3u ? 1 : 0;
-                ctr.nodes += kind != 2u ? 1 : 0;
+                if (a1.w != kSentinelW1) ctr.nodes++;
+                ctr.nodes += cur == f ? 1 : 0;
                 if (wave_leader()) ctr.it_walk++;
             }
-            if (__builtin_expect((ul | ur) != 0, 0)) {  // lanes the f32 margin cannot decide: f64
+            if (__builtin_expect((u1 | u2) != 0, 0)) {  // lanes the f32 margin cannot decide: f64
                 if (COUNT && wave_leader()) ctr.it_slow++;
                 const uint64_t me = 1ull << (threadIdx.x & 63);
-                bool fl = false, fr = false;
-                if (ul & me) {
+                bool f1 = false, f2 = false;
+                if (u1 & me) {
                     if (COUNT) ctr.slow_nodes++;
-                    fl = INVL ? slab64_inv(node64(S, p), o, S.inv64_lds, tmin, R.tmax) : slab64(node64(S, p), o, d, tmin, R.tmax);
+                    f1 = INVL ? slab64_inv(node64(S, f), o, S.inv64_lds, tmin, R.tmax) : slab64(node64(S, f), o, d, tmin, R.tmax);
                 }
-                if (ur & me) {
+                if (u2 & me) {
                     if (COUNT) ctr.slow_nodes++;
-                    fr = INVL ? slab64_inv(node64(S, p + 32), o, S.inv64_lds, tmin, R.tmax)
-                              : slab64(node64(S, p + 32), o, d, tmin, R.tmax);
+                    f2 = INVL ? slab64_inv(node64(S, g), o, S.inv64_lds, tmin, R.tmax) : slab64(node64(S, g), o, d, tmin, R.tmax);
                 }
-                el = (el & ~ul) | __ballot(fl);
-                er = (er & ~ur) | __ballot(fr);
+                e1 = (e1 & ~u1) | __ballot(f1);
+                e2 = (e2 & ~u2) | __ballot(f2);
             }
-            const uint64_t il = __ballot(a1.w < kLeafFlagF), ir = __ballot(b1.w < kLeafFlagF);
-            const uint64_t sent = __ballot(a1.w == kSentinelW1);  // the sentinel is a left child
-            // X: the first entered child in the reference's order (the right one first when sw)
-            const uint64_t xr = er & (sw | ~el);
-            const uint64_t both = el & er, any = el | er;
-            const uint64_t xi = (xr & ir) | (~xr & il);
+            const uint64_t i1 = __ballot(a1.w < kLeafFlagF), i2 = __ballot(b1.w < kLeafFlagF);
+            const uint64_t sent = __ballot(a1.w == kSentinelW1);  // the sentinel is only ever first
+            // X: the first entered node in the reference's order (the first one, else its sibling)
+            const uint64_t both = e1 & e2, any = e1 | e2;
+            const uint64_t xi = (e1 & i1) | (~e1 & i2);
             // an entered leaf: the first one is recorded and the walk goes on with its
-            // continuation (the far token, or the stack top); the second one, and the sentinel,
-            // park as their re-test token (the far token pushed when both were entered)
+            // continuation (the sibling's token, or the stack top); the second one, and the
+            // sentinel, park as their re-test token (the sibling's token pushed when both were
+            // entered)
             const uint64_t leaf = any & ~xi;
-            const uint64_t park = leaf & (~nop | (~xr & sent));
+            const uint64_t park = leaf & (~nop | (e1 & sent));
             const uint64_t dp = (any & xi) | park;  // cur = X's token
-            // the children's tokens: an interior child's own pair in the ray's order, a leaf's
-            // re-test (kind 2 / 3)
-            const uint32_t tokl = vsel(il, __builtin_amdgcn_ubfe(R.neg, a1.z, 1) | a1.w, p | 2u);
-            const uint32_t tokr = vsel(ir, __builtin_amdgcn_ubfe(R.neg, b1.z, 1) | b1.w, p | 3u);
-            const uint32_t tf = vsel(sw, tokl, tokr);  // the far child (pushed when both entered)
-            const uint32_t tx = vsel(xr, tokr, tokl);
+            // the nodes' tokens: an interior node's near child, a leaf's re-test
+            const uint32_t tok1 = vsel(i1, (__builtin_amdgcn_ubfe(R.neg, a1.z, 1) << kNodeFShift) | a1.w, cur | kTokAlone);
+            const uint32_t tok2 = vsel(i2, (__builtin_amdgcn_ubfe(R.neg, b1.z, 1) << kNodeFShift) | b1.w, g | kTokAlone);
+            const uint32_t tx = vsel(e1, tok1, tok2);
             pref = vsel(leaf & nop, tx, pref);
-            tp[stride] = static_cast<SE>(tf);
-            cur = vsel(dp, tx, vsel(both, tf, top));
+            tp[stride] = static_cast<SE>(tok2);
+            cur = vsel(dp, tx, vsel(both, tok2, top));
             tp += (static_cast<int32_t>(vsel(dp, 0u, ~0u)) + static_cast<int32_t>(vsel(both, 1u, 0u))) * stride;
             run = vsel(park, 0u, 1u);
         }
         nop = __ballot(pref == ~0u);
     } while (nop != 0);
     {
-        // the recorded leaf's node: a re-test token's pair, + 32 for the right child (kind 3)
-        const Uvec2 w = fetch_nodef_words<TOP, false>(S, (pref & ~kTokMask) | ((pref & 1u) << 5));
+        const Uvec2 w = fetch_nodef_words<TOP, false>(S, pref & ~kTokAlone);  // the recorded leaf
         R.state = w.y == kSentinelW1 ? kDone : kLeaf;
         R.first = w.x;
         R.count = w.y & ~kLeafFlagF;
@@ -2035,8 +2043,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W5 ? kMa
             // the pair walk's lanes hold tokens (walk_pairs): the root pair's left child, and the
             // sentinel's token in the guard level; rays that need the EXACT walk keep plain refs
             const bool tok = kPair && pw && !(R.neg & kZeroDir);
-            st.base[-static_cast<ptrdiff_t>(st.stride)] = static_cast<SE>(W.sentinel | (tok ? kTokLeft : 0u));
-            if (tok) R.cur = kTokLeft;
+            st.base[-static_cast<ptrdiff_t>(st.stride)] = static_cast<SE>(W.sentinel | (tok ? kTokAlone : 0u));
+            if (tok) R.cur = kTokAlone;
             if (kInvLds) {  // the f64 node test's 1 / d, divided once per ray (slab64_inv)
                 uint32_t t = threadIdx.x;
                 asm volatile("" : "+v"(t));

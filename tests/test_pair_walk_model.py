@@ -1,5 +1,5 @@
-"""A Python model of the sibling-pair walk's state machine (crt_device.hip walk_pairs: tokens,
-skip kinds, the far token pushed or continued, the speculative round that records the first leaf
+"""A Python model of the sibling-pair walk's state machine (crt_device.hip walk_pairs: tokens of
+a first node and its sibling or of one node alone, the sibling's token pushed or continued, the speculative round that records the first leaf
 and parks at the second as a re-test token) against the reference's DFS (bvh.h:617-712). Random
 trees whose node test is monotone in t_max and in containment (a child is entered only where its
 parent is, at any t_max where the parent is: the property the f32 / f64 node test has, walk_pairs'
@@ -46,58 +46,57 @@ def reference(root):
 
 
 def pair_walk(root, stop):
-    """walk_pairs + leaf_step, one lane: token = (pair, kind), kind 0 / 1 both children (1: right
-    first), 2 the left child alone, 3 the right one alone."""
+    """walk_pairs + leaf_step, one lane: token = (first node, alone). Without `alone` the step tests
+    the first node and its sibling (the first one is the near child of their parent); an entered
+    interior node continues as its near child's token, a leaf not processed now as (itself, alone):
+    a re-test of its box."""
     sentinel = {"leaf": True, "near": float("-inf"), "hit": True, "prims": []}
-    pad = {"leaf": True, "near": 0.0, "hit": False, "prims": []}
-    pairs = {"root": [root, pad], "sent": [sentinel, None]}
+    sibling = {}
 
     def reg(n):
         if not n["leaf"]:
-            pairs[id(n)] = n["ch"]
+            a, b = n["ch"]
+            sibling[id(a)], sibling[id(b)] = b, a
             for c in n["ch"]:
                 reg(c)
     reg(root)
 
-    def tok_of(x, pair, is_r):
+    def tok_of(x):
         if x["leaf"]:
-            return (pair, 3 if is_r else 2)
-        return (id(x), 1 if x["sw"] else 0)
+            return (x, True)
+        a, b = x["ch"]
+        return ((b if x["sw"] else a), False)  # the near child, with its sibling
 
-    log, tmax, stack, cur = [], float("inf"), [], ("root", 2)
+    log, tmax, stack, cur = [], float("inf"), [], (root, True)
     while True:
         pref, run = None, True
         while run:
             if pref is not None and stop.random() < 0.3:
                 break  # the wave's loop ends before this lane parks
-            pair, kind = cur
-            L, R = pairs[pair]
-            ml, mr, sw = kind != 3, kind != 2, kind == 1
-            el = ml and enter(L, tmax)
-            er = mr and R is not None and enter(R, tmax)
-            tl = tok_of(L, pair, False)
-            tr = tok_of(R, pair, True) if R is not None else None
-            xr = er and (sw or not el)
-            both, anyc = el and er, el or er
-            X = R if xr else L
+            first, alone = cur
+            second = None if alone else sibling[id(first)]
+            e1 = enter(first, tmax)
+            e2 = second is not None and enter(second, tmax)
+            t1 = tok_of(first) if not first["leaf"] else (first, True)
+            t2 = tok_of(second) if second is not None else None
+            both, anyc = e1 and e2, e1 or e2
+            X = first if e1 else second
             xi = anyc and not X["leaf"]
             leaf = anyc and X["leaf"]
-            park = leaf and (pref is not None or ((not xr) and L is sentinel))
-            tf = tl if sw else tr
-            tx = tr if xr else tl
+            park = leaf and (pref is not None or (e1 and first is sentinel))
+            tx = t1 if e1 else t2
             if leaf and pref is None:
                 pref = tx
             if xi or park:
                 cur = tx
                 if both:
-                    stack.append(tf)
+                    stack.append(t2)
             elif both:
-                cur = tf
+                cur = t2
             else:
-                cur = stack.pop() if stack else ("sent", 2)  # the guard level
+                cur = stack.pop() if stack else (sentinel, True)  # the guard level
             run = not park
-        pair, kind = pref
-        node = pairs[pair][1 if kind == 3 else 0]
+        node = pref[0]
         if node is sentinel:
             return log
         log.append((id(node), tmax))
