@@ -1013,40 +1013,7 @@ __device__ __forceinline__ Uvec2 fetch_nodef_words(const SceneView& S, uint32_t 
     return w;
 }
 
-// The f32 decision of a node that is flat on an axis k (its two f32 slab values there are equal:
-// every Box face and Cornell wall, box.h:53-84, lies on a leaf's or a node's bounds). The general
-// test (walk) cannot decide such nodes: near and far both contain t_k, so gap' = hi' - lo' is 0
-// for every ray that meets the face inside its extent, and Cornell decided 28% of its walk
-// iterations in f64. Treated as a point, t_k decides: with lo2 = max(near_i, near_j, tmin) and
-// hi2 = min(far_i, far_j, tmax) over the other two axes (f32, as in walk), and th = 2^-19 M + marg,
-// M = max(|lo2'|, |hi2'|, |t_k'|):
-//   t_k' - lo2' > th and hi2' - t_k' > th  =>  enter,
-//   t_k' - lo2' < -th or hi2' - t_k' < -th or hi2' - lo2' < -th  =>  miss.
-// Each comparison is one subtraction of two approximated slab values (or tmin' / tmax'), the
-// quantity walk()'s bound covers with the same th; and both f64 slab values of axis k (near_k <=
-// far_k: NaN-free rays, non-inverted boxes) are within that bound of t_k', so "enter" gives
-// near_i <= lo2 < near_k <= far_k < hi2 <= far_j for every pair of axes (near <= far), near < tmax,
-// far > tmin, and each "miss" gives one of near > far, far <= tmin, near >= tmax in f64. A node
-// flat on two axes stays undecided (hi2 ~ lo2) and goes to f64 as before. Returns 1 enter, 0 miss,
-// -1 undecided.
-__device__ __forceinline__ int flat_decide(float x0, float x1, float y0, float y1, float z0, float z1,
-                                           float tmin32, float tmax32, float marg) {
-    const bool fx = x0 == x1, fy = y0 == y1, fz = z0 == z1;
-    if (!(fx | fy | fz)) return -1;
-    const float t = fx ? x0 : fy ? y0 : z0;
-    const float a0 = fx ? y0 : x0, a1 = fx ? y1 : x1;
-    const float b0 = (fx | fy) ? z0 : y0, b1 = (fx | fy) ? z1 : y1;
-    const float lo2 = vmax3(vmin(a0, a1), vmin(b0, b1), tmin32);
-    const float hi2 = vmin3(vmax(a0, a1), vmax(b0, b1), tmax32);
-    const float m = __builtin_fmaxf(vmax_abs(lo2, hi2), __builtin_fabsf(t));
-    const float th = __builtin_fmaf(m, 0x1p-19f, marg);
-    const float d1 = t - lo2, d2 = hi2 - t, d3 = hi2 - lo2;
-    if ((d1 > th) & (d2 > th)) return 1;
-    if ((d1 < -th) | (d2 < -th) | (d3 < -th)) return 0;
-    return -1;
-}
-
-template <typename SE, bool COUNT, bool EXACT, bool TOP, bool LS, bool GS, bool SPEC, bool INVL = false, bool FLATD = false>
+template <typename SE, bool COUNT, bool EXACT, bool TOP, bool LS, bool GS, bool SPEC, bool INVL = false>
 __device__ __forceinline__ void walk(const SceneView& S, Stack<SE>& st, const double o[3], const double d[3],
                                      double tmin, float tmin32, Trav& R, LaneCounters& ctr) {
     // Every step ends with the next node in `cur`: the near child of an entered interior node,
@@ -1156,20 +1123,13 @@ __device__ __forceinline__ void walk(const SceneView& S, Stack<SE>& st, const do
                 const float gap = hi - lo;
                 const float th = __builtin_fmaf(vmax_abs(lo, hi), 0x1p-19f, R.marg);
                 bool enter = gap > 0.f;
-                bool unc = !(fabsf(gap) > th);
+                const bool unc = !(fabsf(gap) > th);
                 if (__builtin_expect(__ballot(unc) != 0, 0)) {
-                    if (FLATD && unc) {  // nodes flat on an axis: decided in f32 as a point
-                        const int f = flat_decide(x0, x1, y0, y1, z0, z1, tmin32, R.tmax32, R.marg);
-                        enter = f > 0;
-                        unc = f < 0;
-                    }
-                    if (!FLATD || __ballot(unc) != 0) {
-                        if (COUNT && wave_leader()) ctr.it_slow++;
-                        if (unc) {
-                            if (COUNT) ctr.slow_nodes++;
-                            enter = INVL ? slab64_inv(node64(S, cur), o, S.inv64_lds, tmin, R.tmax)
-                                         : slab64(node64(S, cur), o, d, tmin, R.tmax);
-                        }
+                    if (COUNT && wave_leader()) ctr.it_slow++;
+                    if (unc) {
+                        if (COUNT) ctr.slow_nodes++;
+                        enter = INVL ? slab64_inv(node64(S, cur), o, S.inv64_lds, tmin, R.tmax)
+                                     : slab64(node64(S, cur), o, d, tmin, R.tmax);
                     }
                 }
                 const bool inner = enter & (w1 < kLeafFlagF);
@@ -1226,20 +1186,13 @@ __device__ __forceinline__ void walk(const SceneView& S, Stack<SE>& st, const do
             const float gap = hi - lo;
             const float th = __builtin_fmaf(vmax_abs(lo, hi), 0x1p-19f, R.marg);
             bool enter = gap > 0.f;
-            bool unc = !(fabsf(gap) > th);
+            const bool unc = !(fabsf(gap) > th);
             if (__builtin_expect(__ballot(unc) != 0, 0)) {
-                if (FLATD && unc) {  // nodes flat on an axis: decided in f32 as a point
-                    const int f = flat_decide(x0, x1, y0, y1, z0, z1, tmin32, R.tmax32, R.marg);
-                    enter = f > 0;
-                    unc = f < 0;
-                }
-                if (!FLATD || __ballot(unc) != 0) {
-                    if (COUNT && wave_leader()) ctr.it_slow++;
-                    if (unc) {
-                        if (COUNT) ctr.slow_nodes++;
-                        enter = INVL ? slab64_inv(node64(S, cur), o, S.inv64_lds, tmin, R.tmax)
-                                     : slab64(node64(S, cur), o, d, tmin, R.tmax);
-                    }
+                if (COUNT && wave_leader()) ctr.it_slow++;
+                if (unc) {
+                    if (COUNT) ctr.slow_nodes++;
+                    enter = INVL ? slab64_inv(node64(S, cur), o, S.inv64_lds, tmin, R.tmax)
+                                 : slab64(node64(S, cur), o, d, tmin, R.tmax);
                 }
             }
             const bool inner = enter & (w1 < kLeafFlagF);
@@ -1300,9 +1253,6 @@ __device__ __forceinline__ void walk(const SceneView& S, Stack<SE>& st, const do
 // the reference's DFS on random trees.
 #ifndef CRT_PAIR_WALK
 #define CRT_PAIR_WALK 0
-#endif
-#ifndef CRT_FLAT_DECIDE
-#define CRT_FLAT_DECIDE 0
 #endif
 constexpr uint32_t kTokAlone = 1u;  // token bit 0: the first node alone (root, sentinel, re-tests)
 
@@ -1936,8 +1886,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W5 ? kMa
     // the sibling-pair walk (walk_pairs) of the HBM-scene instances; the instrumented pass walks
     // that way only when it walks like the timed kernel (CRT_COUNT_SPEC=1)
     constexpr bool kPair = CRT_PAIR_WALK && !LSCENE;
-    // the flat-node f32 decision (flat_decide) in the instances that can meet parallelograms
-    constexpr bool kFlatD = CRT_FLAT_DECIDE && PM != 0;
     const bool pw = kPair && W.pair_walk && (!COUNT || W.count_spec);
     S.inv64_lds = W.lds_inv64;
     if (kAccLds) {
@@ -2083,9 +2031,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W5 ? kMa
             } else if (!W.exact_slab && __ballot(R.state == kWalk && (R.neg & kZeroDir)) == 0) {
                 if (R.state == kWalk) {
                     if (!COUNT || W.count_spec)
-                        walk<SE, COUNT, false, kTopTreelet && !LSCENE, LSCENE, GSTACK, true, kInvLds, kFlatD>(S, st, P.o, P.d, C.t_min, tmin32, R, ctr);
+                        walk<SE, COUNT, false, kTopTreelet && !LSCENE, LSCENE, GSTACK, true, kInvLds>(S, st, P.o, P.d, C.t_min, tmin32, R, ctr);
                     else
-                        walk<SE, COUNT, false, kTopTreelet && !LSCENE, LSCENE, GSTACK, false, kInvLds, kFlatD>(S, st, P.o, P.d, C.t_min, tmin32, R, ctr);
+                        walk<SE, COUNT, false, kTopTreelet && !LSCENE, LSCENE, GSTACK, false, kInvLds>(S, st, P.o, P.d, C.t_min, tmin32, R, ctr);
                 }
             } else {
                 if (R.state == kWalk) walk<SE, COUNT, true, kTopTreelet && !LSCENE, LSCENE, GSTACK, false>(S, st, P.o, P.d, C.t_min, tmin32, R, ctr);
@@ -3297,7 +3245,7 @@ const char* device_build_info() {
     return "arch=" CRT_ARCH " CRT_BLOCK=" CRT_STR(CRT_BLOCK) " CRT_TILE_W=" CRT_STR(CRT_TILE_W)
            " CRT_WAVES_PER_EU=" CRT_STR(CRT_WAVES_PER_EU) " CRT_WAVES_PER_EU_LDS=" CRT_STR(CRT_WAVES_PER_EU_LDS)
            " CRT_SHADE_BATCH=" CRT_STR(CRT_SHADE_BATCH) " CRT_CHUNK_MIN=" CRT_STR(CRT_CHUNK_MIN)
-           " CRT_WATCHDOG=" CRT_STR(CRT_WATCHDOG) " CRT_PAIR_WALK=" CRT_STR(CRT_PAIR_WALK) " CRT_FLAT_DECIDE=" CRT_STR(CRT_FLAT_DECIDE);
+           " CRT_WATCHDOG=" CRT_STR(CRT_WATCHDOG) " CRT_PAIR_WALK=" CRT_STR(CRT_PAIR_WALK);
 }
 
 }  // namespace crt
