@@ -52,6 +52,14 @@ constexpr int kBlock = CRT_BLOCK;
 constexpr uint32_t kTileW = CRT_TILE_W, kTileH = 64 / CRT_TILE_W;
 // waves per SIMD of the W5 instances (the "five-wave" ones)
 constexpr int kManyWaves = 5;
+// the HBM-scene instances' sibling-pair walk (walk_pairs; 0 builds the one-node walk for A/B) and
+// two-record leaf filter rounds (measured level, off)
+#ifndef CRT_PAIR_WALK
+#define CRT_PAIR_WALK 1
+#endif
+#ifndef CRT_LEAF_UNROLL
+#define CRT_LEAF_UNROLL 0
+#endif
 constexpr double kScale = 1 / static_cast<double>(4294967295u - 1);  // rand_util.h:110-112
 
 typedef double Dvec2 __attribute__((ext_vector_type(2)));
@@ -414,11 +422,6 @@ __device__ __forceinline__ float vmax_abs(float a, float b) {
 __device__ __forceinline__ float vmax3_0(float a, float b) {  // max(a, b, 0)
     float r;
     asm("v_max3_f32 %0, %1, %2, 0" : "=v"(r) : "v"(a), "v"(b));
-    return r;
-}
-__device__ __forceinline__ float vmed3(float a, float b, float c) {
-    float r;
-    asm("v_med3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
     return r;
 }
 __device__ __forceinline__ float vmax3(float a, float b, float c) {
@@ -869,12 +872,7 @@ __device__ __forceinline__ void trav_init(const double o[3], const double d[3], 
 //   gap' >  th  =>  gap > 0: far > near, near < tmax, far > tmin  (enter)
 //   gap' < -th  =>  gap < 0: far < near, far < tmin or tmax < near (no entry)
 // and only lanes with |gap'| <= th (grazing rays, ties, rays with marg = inf) run the f64 test on
-// the f64 node.
-// hi' takes med3(z0', z1', tmax') for min(max(z0', z1'), tmax') (one instruction fewer a node,
-// round 6): they differ only when tmax' < min(z0', z1'), and then lo' >= min(z0', z1') >= hi', so
-// gap' <= 0 is never "enter"; a "miss" has gap'(std) <= gap' < -th, and th is no smaller than the
-// standard one (hi' >= hi'(std) > 0 where they differ, else hi' equals it), so the standard
-// bound still proves it. Every decision is the f64 test's, so each ray visits the reference's node
+// the f64 node. Every decision is the f64 test's, so each ray visits the reference's node
 // sequence. The f32 test is 18 single-rate instructions where the f64 one is 25 half-rate ones.
 typedef __attribute__((address_space(3))) const unsigned char LdsByte;
 struct NodeLines {
@@ -1119,7 +1117,7 @@ __device__ __forceinline__ void walk(const SceneView& S, Stack<SE>& st, const do
                 const float z0 = __builtin_fmaf(__uint_as_float(q1.x), R.inv32[2], -R.oinv32[2]);
                 const float z1 = __builtin_fmaf(__uint_as_float(q1.y), R.inv32[2], -R.oinv32[2]);
                 const float lo = vmax3(vmin(x0, x1), vmin(y0, y1), vmax_s(vmin(z0, z1), tmin32));
-                const float hi = vmin3(vmax(x0, x1), vmax(y0, y1), vmed3(z0, z1, R.tmax32));
+                const float hi = vmin3(vmax(x0, x1), vmax(y0, y1), vmin(vmax(z0, z1), R.tmax32));
                 const float gap = hi - lo;
                 const float th = __builtin_fmaf(vmax_abs(lo, hi), 0x1p-19f, R.marg);
                 bool enter = gap > 0.f;
@@ -1182,7 +1180,7 @@ __device__ __forceinline__ void walk(const SceneView& S, Stack<SE>& st, const do
             const float z0 = __builtin_fmaf(__uint_as_float(q1.x), R.inv32[2], -R.oinv32[2]);
             const float z1 = __builtin_fmaf(__uint_as_float(q1.y), R.inv32[2], -R.oinv32[2]);
             const float lo = vmax3(vmin(x0, x1), vmin(y0, y1), vmax_s(vmin(z0, z1), tmin32));
-            const float hi = vmin3(vmax(x0, x1), vmax(y0, y1), vmed3(z0, z1, R.tmax32));
+            const float hi = vmin3(vmax(x0, x1), vmax(y0, y1), vmin(vmax(z0, z1), R.tmax32));
             const float gap = hi - lo;
             const float th = __builtin_fmaf(vmax_abs(lo, hi), 0x1p-19f, R.marg);
             bool enter = gap > 0.f;
@@ -1251,9 +1249,7 @@ __device__ __forceinline__ void walk(const SceneView& S, Stack<SE>& st, const do
 // | 1: its "sibling", past the node array, is never tested). The root's token is 0 | 1 (the pad
 // node beside it is never tested). tests/test_pair_walk_model.py runs this state machine against
 // the reference's DFS on random trees.
-#ifndef CRT_PAIR_WALK
-#define CRT_PAIR_WALK 0
-#endif
+
 constexpr uint32_t kTokAlone = 1u;  // token bit 0: the first node alone (root, sentinel, re-tests)
 
 // v_cndmask_b32 with a lane mask from a ballot (scalar registers): m ? a : b per lane
@@ -1263,6 +1259,9 @@ __device__ __forceinline__ uint32_t vsel(uint64_t m, uint32_t a, uint32_t b) {
     return r;
 }
 
+// The step's two f32 nodes: f (the first) and g = f ^ 32, read from the LDS treelet or from HBM
+// (the treelet holds whole sibling pairs, dispatch_render, so f and g are on the same side),
+// both sides in flight together as in fetch_nodef.
 // The step's two f32 nodes: f (the first) and g = f ^ 32, read from the LDS treelet or from HBM
 // (the treelet holds whole sibling pairs, dispatch_render, so f and g are on the same side),
 // both sides in flight together as in fetch_nodef.
@@ -1302,19 +1301,22 @@ __device__ __forceinline__ void fetch_two(const SceneView& S, uint32_t f, uint32
     }
 }
 
-// the f32 node test of walk() on one child: gap' = hi' - lo' and its threshold
-__device__ __forceinline__ void child_gap(const Uvec4& q0, const Uvec4& q1, const Trav& R, float tmin32, float& gap,
-                                          float& th) {
+// the f32 node test of walk() on one node: lo' = max(near', tmin'), hi' = min(far', tmax')
+__device__ __forceinline__ void node_lohi(const Uvec4& q0, const Uvec4& q1, const Trav& R, float tmin32, float& lo,
+                                          float& hi) {
     const float x0 = __builtin_fmaf(__uint_as_float(q0.x), R.inv32[0], -R.oinv32[0]);
     const float x1 = __builtin_fmaf(__uint_as_float(q0.y), R.inv32[0], -R.oinv32[0]);
     const float y0 = __builtin_fmaf(__uint_as_float(q0.z), R.inv32[1], -R.oinv32[1]);
     const float y1 = __builtin_fmaf(__uint_as_float(q0.w), R.inv32[1], -R.oinv32[1]);
     const float z0 = __builtin_fmaf(__uint_as_float(q1.x), R.inv32[2], -R.oinv32[2]);
     const float z1 = __builtin_fmaf(__uint_as_float(q1.y), R.inv32[2], -R.oinv32[2]);
-    const float lo = vmax3(vmin(x0, x1), vmin(y0, y1), vmax_s(vmin(z0, z1), tmin32));
-    const float hi = vmin3(vmax(x0, x1), vmax(y0, y1), vmed3(z0, z1, R.tmax32));
-    gap = hi - lo;
-    th = __builtin_fmaf(vmax_abs(lo, hi), 0x1p-19f, R.marg);
+    lo = vmax3(vmin(x0, x1), vmin(y0, y1), vmax_s(vmin(z0, z1), tmin32));
+    hi = vmin3(vmax(x0, x1), vmax(y0, y1), vmin(vmax(z0, z1), R.tmax32));
+}
+__device__ __forceinline__ float vmax3_abs(float a, float b, float c) {
+    float r;
+    asm("v_max3_f32 %0, |%1|, |%2|, |%3|" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
 }
 
 template <typename SE, bool COUNT, bool TOP, bool INVL>
@@ -1328,7 +1330,9 @@ __device__ __forceinline__ void walk_pairs(const SceneView& S, Stack<SE>& st, co
     uint32_t pref = ~0u;  // the first leaf's re-test token (or the sentinel's), ~0u: none yet
     // The per-lane logic is written on lane masks (uint64_t ballots: scalar ALU) with v_cndmask
     // selects (vsel); as bools across the rare f64 branch, the compiler materialises the
-    // conditions as 0 / 1 in VGPRs and spends ~40 VALU a step on them.
+    // conditions as 0 / 1 in VGPRs and spends ~40 VALU a step on them. (The loop state as masks
+    // too, with a wave-uniform body and masked updates: 65 VALU a step instead of 69, but config 4
+    // 128.9-129.4 vs 127.7-127.8 ms, profiles/r06_pair_tuning.)
     uint64_t nop = __ballot(true);  // lanes with no leaf recorded yet
     do {
         CRT_WD(7, cur, static_cast<uint32_t>(tp - empty));
@@ -1337,9 +1341,15 @@ __device__ __forceinline__ void walk_pairs(const SceneView& S, Stack<SE>& st, co
             Uvec4 a0, a1, b0, b1;
             fetch_two<TOP>(S, f, g, a0, a1, b0, b1);
             const uint32_t top = *tp;  // speculative pop
-            float g1, t1, g2, t2;
-            child_gap(a0, a1, R, tmin32, g1, t1);
-            child_gap(b0, b1, R, tmin32, g2, t2);
+            float lo1, hi1, lo2, hi2;
+            node_lohi(a0, a1, R, tmin32, lo1, hi1);
+            node_lohi(b0, b1, R, tmin32, lo2, hi2);
+            const float g1 = hi1 - lo1, g2 = hi2 - lo2;
+            // one threshold for both nodes: walk()'s bound holds for any M at least each node's
+            // own max(|lo'|, |hi'|) (v_max ignores a NaN operand; a node tested alone has a sibling
+            // of finite bounds, except the sentinel's, past the node array: at worst its step is
+            // decided in f64)
+            const float t1 = __builtin_fmaf(vmax_abs(vmax3_abs(lo1, hi1, lo2), hi2), 0x1p-19f, R.marg), t2 = t1;
             const uint64_t two = __ballot(cur == f);  // the sibling is tested too
             uint64_t e1 = __ballot(g1 > 0.f), e2 = __ballot(g2 > 0.f) & two;
             const uint64_t u1 = __ballot(!(fabsf(g1) > t1)), u2 = two & __ballot(!(fabsf(g2) > t2));
@@ -1432,6 +1442,28 @@ __device__ __forceinline__ void leaf_step(const SceneView& S, Stack<SE>& st, con
                     if (wave_leader()) ctr.it_leaf += 2;
                 }
                 cand = sphere_pair_candidates(cand, pair_at((LdsPair*)static_cast<uintptr_t>(S.spair_lds + ((range.x + i) << 5))), L);
+            }
+        } else if (CRT_LEAF_UNROLL) {
+            // HBM records: two a round (records i and i + 2, both in the leaf), their loads in
+            // flight together, one wait; then the last record of an odd record count. One loop
+            // waited a memory latency per record (config 4's pass 1)
+            uint32_t i = 0;
+            for (; i + 2 < range.y; i += 4) {
+                const DevSpherePair r0 = pair_at((GlobalPair*)(S.spair + range.x + i));
+                const DevSpherePair r1 = pair_at((GlobalPair*)(S.spair + range.x + i + 2));
+                if (COUNT) {
+                    ctr.sphere_tests += i + 3 < range.y ? 4 : 3;
+                    if (wave_leader()) ctr.it_leaf += 4;
+                }
+                cand = sphere_pair_candidates(cand, r0, L);
+                cand = sphere_pair_candidates(cand, r1, L);
+            }
+            if (i < range.y) {
+                if (COUNT) {
+                    ctr.sphere_tests += i + 1 < range.y ? 2 : 1;
+                    if (wave_leader()) ctr.it_leaf += 2;
+                }
+                cand = sphere_pair_candidates(cand, pair_at((GlobalPair*)(S.spair + range.x + i)), L);
             }
         } else {
             for (uint32_t i = 0; i < range.y; i += 2) {
@@ -3245,7 +3277,7 @@ const char* device_build_info() {
     return "arch=" CRT_ARCH " CRT_BLOCK=" CRT_STR(CRT_BLOCK) " CRT_TILE_W=" CRT_STR(CRT_TILE_W)
            " CRT_WAVES_PER_EU=" CRT_STR(CRT_WAVES_PER_EU) " CRT_WAVES_PER_EU_LDS=" CRT_STR(CRT_WAVES_PER_EU_LDS)
            " CRT_SHADE_BATCH=" CRT_STR(CRT_SHADE_BATCH) " CRT_CHUNK_MIN=" CRT_STR(CRT_CHUNK_MIN)
-           " CRT_WATCHDOG=" CRT_STR(CRT_WATCHDOG) " CRT_PAIR_WALK=" CRT_STR(CRT_PAIR_WALK);
+           " CRT_WATCHDOG=" CRT_STR(CRT_WATCHDOG) " CRT_PAIR_WALK=" CRT_STR(CRT_PAIR_WALK) " CRT_LEAF_UNROLL=" CRT_STR(CRT_LEAF_UNROLL);
 }
 
 }  // namespace crt
