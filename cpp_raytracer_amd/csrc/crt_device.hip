@@ -1392,7 +1392,8 @@ __device__ __forceinline__ void walk_pairs(const SceneView& S, Stack<SE>& st, co
             pref = vsel(leaf & nop, tx, pref);
             tp[stride] = static_cast<SE>(tok2);
             cur = vsel(dp, tx, vsel(both, tok2, top));
-            tp += (static_cast<int32_t>(vsel(dp, 0u, ~0u)) + static_cast<int32_t>(vsel(both, 1u, 0u))) * stride;
+            // one level up when the walk descends with both entered, one down when it pops
+            tp += static_cast<int32_t>(vsel(dp & both, 1u, vsel(~dp & ~both, ~0u, 0u))) * stride;
             run = vsel(park, 0u, 1u);
         }
         nop = __ballot(pref == ~0u);
