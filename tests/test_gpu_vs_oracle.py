@@ -313,3 +313,27 @@ def test_five_wave_instance_equals_four_wave(crt, monkeypatch, name, seed, kw):
     check(five, orc.render(d, 70, threads=8))
     monkeypatch.setenv("CRT_FOUR_WAVES", "1")
     assert np.array_equal(five, gpu(crt, d, 70))
+
+
+@pytest.mark.parametrize("name,seed,kw", [
+    ("christmas_tree", None, dict(image_w=96, image_h=54, samples_per_pixel=6)),
+    ("rtow_final", 42, dict(image_w=96, image_h=64, samples_per_pixel=4, max_depth=50)),
+    ("cornell", None, dict(image_w=64, image_h=64, samples_per_pixel=4, max_depth=200)),
+    ("millions", 42, dict(image_w=64, image_h=36, samples_per_pixel=4, max_depth=20)),
+])
+def test_pair_walk_equals_node_walk(crt, monkeypatch, name, seed, kw):
+    """The HBM-scene kernels' sibling-pair walk (walk_pairs, round 6) against the one-node walk it
+    replaced (CRT_NO_PAIR_WALK=1): the same primitive tests in the same order with the same t_max,
+    so bit-identical frames, on scenes forced into HBM (CRT_NO_LDS_SCENE) and on millions (4202 to
+    2.1 M primitives, sphere-only and parallelogram instances), and the GPU frame equals the oracle's."""
+    monkeypatch.setenv("CRT_NO_LDS_SCENE", "1")
+    d = scene(crt, name, seed, **kw)
+    s = crt.GpuScene(d, build_device=0 if name == "millions" else None)
+    cam = crt.resolve_camera(d.camera, 41)
+    pair, _ = s.render(cam, 1)
+    monkeypatch.setenv("CRT_NO_PAIR_WALK", "1")
+    node, _ = s.render(cam, 1)
+    assert pair.tobytes() == node.tobytes()
+    assert s.guard(0) == 0
+    if name != "millions":  # the oracle's millions build alone takes ~10 s
+        check(pair, orc.render(d, 41, threads=8))
