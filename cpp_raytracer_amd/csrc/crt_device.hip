@@ -1011,7 +1011,7 @@ __device__ __forceinline__ Uvec2 fetch_nodef_words(const SceneView& S, uint32_t 
     return w;
 }
 
-template <typename SE, bool COUNT, bool EXACT, bool TOP, bool LS, bool GS, bool SPEC, bool INVL = false>
+template <typename SE, bool COUNT, bool EXACT, bool TOP, bool LS, bool GS, bool SPEC, bool INVL = false, bool G2 = true>
 __device__ __forceinline__ void walk(const SceneView& S, Stack<SE>& st, const double o[3], const double d[3],
                                      double tmin, float tmin32, Trav& R, LaneCounters& ctr) {
     // Every step ends with the next node in `cur`: the near child of an entered interior node,
@@ -1134,7 +1134,12 @@ __device__ __forceinline__ void walk(const SceneView& S, Stack<SE>& st, const do
                 const uint32_t near = w1 | (__builtin_amdgcn_ubfe(R.neg, w0, 1) << kNodeFShift);
                 tp[stride] = static_cast<SE>(near ^ (1u << kNodeFShift));
                 const bool reached = enter & !inner;  // a leaf or the sentinel
-                const bool park = reached & (!nopend | (w1 == kSentinelW1));
+                // a lane that reaches the sentinel with no leaf recorded records it and pops the
+                // second guard level, which holds the sentinel too: it parks there, with a leaf
+                // recorded (one compare fewer a step than testing for the sentinel here; G2 =
+                // false: the compare, for the flat-parallelogram instances, whose five-wave
+                // register allocation spilled 14 VGPRs instead of 8 without it)
+                const bool park = reached & (!nopend | (!G2 && w1 == kSentinelW1));
                 pref = (reached & nopend) ? cur : pref;  // the first leaf (or the sentinel)
                 pcur = park ? cur : pcur;
                 run = !park;
@@ -1374,16 +1379,15 @@ __device__ __forceinline__ void walk_pairs(const SceneView& S, Stack<SE>& st, co
                 e2 = (e2 & ~u2) | __ballot(f2);
             }
             const uint64_t i1 = __ballot(a1.w < kLeafFlagF), i2 = __ballot(b1.w < kLeafFlagF);
-            const uint64_t sent = __ballot(a1.w == kSentinelW1);  // the sentinel is only ever first
             // X: the first entered node in the reference's order (the first one, else its sibling)
             const uint64_t both = e1 & e2, any = e1 | e2;
             const uint64_t xi = (e1 & i1) | (~e1 & i2);
             // an entered leaf: the first one is recorded and the walk goes on with its
-            // continuation (the sibling's token, or the stack top); the second one, and the
-            // sentinel, park as their re-test token (the sibling's token pushed when both were
-            // entered)
+            // continuation (the sibling's token, or the stack top); the second one parks as its
+            // re-test token (the sibling's token pushed when both were entered). The sentinel is
+            // recorded like a leaf and met again on the second guard level, where the lane parks.
             const uint64_t leaf = any & ~xi;
-            const uint64_t park = leaf & (~nop | (e1 & sent));
+            const uint64_t park = leaf & ~nop;  // the sentinel: recorded, then met again below the guard
             const uint64_t dp = (any & xi) | park;  // cur = X's token
             // the nodes' tokens: an interior node's near child, a leaf's re-test
             const uint32_t tok1 = vsel(i1, (__builtin_amdgcn_ubfe(R.neg, a1.z, 1) << kNodeFShift) | a1.w, cur | kTokAlone);
@@ -1884,18 +1888,18 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W5 ? kMa
     const uint32_t lane = threadIdx.x & 63;
     LaneCounters ctr{};
     const unsigned long long t_start = COUNT ? wall_clock64() : 0;
-    // stack levels 0..depth of this lane, above a guard level holding the sentinel reference
-    // and one more level walk() may read (two guard levels in HBM; in LDS the level below the
-    // guard is other data)
+    // stack levels 0..depth of this lane, above two guard levels holding the sentinel reference
+    // and one more level walk() may read (three levels in HBM; in LDS that one is other data)
     Stack<SE> st;
     if (GSTACK) {
         st.stride = gridDim.x * kBlock;
-        st.base = gstack + (static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x) + 2 * static_cast<size_t>(st.stride);
+        st.base = gstack + (static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x) + 3 * static_cast<size_t>(st.stride);
     } else {
         st.base = reinterpret_cast<SE*>(smem + W.lds_stack) + threadIdx.x;
         st.stride = kBlock;
     }
     st.base[-static_cast<ptrdiff_t>(st.stride)] = static_cast<SE>(W.sentinel);
+    st.base[-2 * static_cast<ptrdiff_t>(st.stride)] = static_cast<SE>(W.sentinel);
     // The wave's current item (wave-uniform) and how many of its 64 units are drawn; lanes take
     // the next units in lane order. A unit's sum goes to partial[chunk][pixel] whichever lane
     // traced it, so frames do not depend on the schedule.
@@ -2025,6 +2029,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W5 ? kMa
             // sentinel's token in the guard level; rays that need the EXACT walk keep plain refs
             const bool tok = kPair && pw && !(R.neg & kZeroDir);
             st.base[-static_cast<ptrdiff_t>(st.stride)] = static_cast<SE>(W.sentinel | (tok ? kTokAlone : 0u));
+            if (!kFlatOnly) st.base[-2 * static_cast<ptrdiff_t>(st.stride)] = static_cast<SE>(W.sentinel | (tok ? kTokAlone : 0u));
             if (tok) R.cur = kTokAlone;
             if (kInvLds) {  // the f64 node test's 1 / d, divided once per ray (slab64_inv)
                 uint32_t t = threadIdx.x;
@@ -2064,7 +2069,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W5 ? kMa
             } else if (!W.exact_slab && __ballot(R.state == kWalk && (R.neg & kZeroDir)) == 0) {
                 if (R.state == kWalk) {
                     if (!COUNT || W.count_spec)
-                        walk<SE, COUNT, false, kTopTreelet && !LSCENE, LSCENE, GSTACK, true, kInvLds>(S, st, P.o, P.d, C.t_min, tmin32, R, ctr);
+                        walk<SE, COUNT, false, kTopTreelet && !LSCENE, LSCENE, GSTACK, true, kInvLds, !kFlatOnly>(S, st, P.o, P.d, C.t_min, tmin32, R, ctr);
                     else
                         walk<SE, COUNT, false, kTopTreelet && !LSCENE, LSCENE, GSTACK, false, kInvLds>(S, st, P.o, P.d, C.t_min, tmin32, R, ctr);
                 }
@@ -2638,7 +2643,7 @@ static int launch_render(const crt_scene* s, int device, const crt_camera* cam, 
     if (!count)
         HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&partial), band_px * 3 * W.chunks * sizeof(double), stream));
     if (GSTACK) {
-        size_t bytes = static_cast<size_t>(s->depth + 3) * resident * dev::kBlock * sizeof(SE);  // + 2 guard levels
+        size_t bytes = static_cast<size_t>(s->depth + 4) * resident * dev::kBlock * sizeof(SE);  // + 3 levels below
         HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&gstack), bytes, stream));
     }
     if (count) {
@@ -2789,15 +2794,16 @@ static int dispatch_render(const crt_scene* s, int device, const crt_camera* cam
     W.f32_ok = s->dev[device].f32_ok ? 1u : 0u;
     W.tmin32 = static_cast<float>(cam->t_min);
     const bool force_global = std::getenv("CRT_NO_LDS_SCENE") != nullptr;
-    // LDS stacks: [data][guard level: sentinel][levels 0..depth]. walk() reads the level below the
-    // guard (the speculative pop at the sentinel) and, at a walk's exit after the sentinel, its
-    // stack pointer stands one level lower still: the guard starts at least two levels into the
-    // allocation, so every level the pointer reaches has a non-negative LDS address. (With one
+    // LDS stacks: [data][second guard: sentinel][guard level: sentinel][levels 0..depth]. A lane
+    // that reaches the sentinel with no leaf recorded pops the second guard (round 6: it holds the
+    // sentinel too, so the walks need no sentinel compare), and the speculative read reaches one
+    // level below it: the guard starts at least three levels into the allocation and the second
+    // guard lies past the data, so every level the pointer reaches has a non-negative LDS address. (With one
     // level, a 640-thread block on a small scene put that pointer at a negative address; the
     // level count derived from it then wrapped, and the flat-parallelogram instance walked a
     // garbage stack forever: the round-4 hang, found with -DCRT_WATCHDOG=1. Power-of-two blocks
     // had wrapped back onto the right level by the modular arithmetic alone.)
-    auto stack_at = [&](size_t data_bytes) { return static_cast<uint32_t>(std::max<size_t>(data_bytes, 2 * level) + level); };
+    auto stack_at = [&](size_t data_bytes) { return static_cast<uint32_t>(std::max<size_t>(data_bytes, 2 * level) + 2 * level); };
     if (!force_global && stack_at(scene_bytes) + stack_bytes <= kLdsSceneBudget) {
         W.lds_nodes = 0;
         W.lds_refs = W.lds_nodes + W.bytes_nodes;
@@ -2840,7 +2846,7 @@ static int dispatch_render(const crt_scene* s, int device, const crt_camera* cam
         return no_top ? 0u : static_cast<uint32_t>(std::min(all_nodes, room / (2 * sizeof(DevNodeF)) * (2 * sizeof(DevNodeF))));
     };
     if (stack_bytes <= kLdsStackBudget && std::getenv("CRT_FORCE_GSTACK") == nullptr) {
-        const size_t taken = stack_bytes + 2 * level + kInvBytes;
+        const size_t taken = stack_bytes + 3 * level + kInvBytes;
         const size_t room = per_block > taken ? per_block - taken : 0;
         W.ntop = top_bytes(room);
         W.lds_nodes = 0;
