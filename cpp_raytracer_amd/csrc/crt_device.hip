@@ -52,13 +52,9 @@ constexpr int kBlock = CRT_BLOCK;
 constexpr uint32_t kTileW = CRT_TILE_W, kTileH = 64 / CRT_TILE_W;
 // waves per SIMD of the W5 instances (the "five-wave" ones)
 constexpr int kManyWaves = 5;
-// the HBM-scene instances' sibling-pair walk (walk_pairs; 0 builds the one-node walk for A/B) and
-// two-record leaf filter rounds (measured level, off)
+// the HBM-scene instances' sibling-pair walk (walk_pairs; 0 builds the one-node walk for A/B)
 #ifndef CRT_PAIR_WALK
 #define CRT_PAIR_WALK 1
-#endif
-#ifndef CRT_LEAF_UNROLL
-#define CRT_LEAF_UNROLL 0
 #endif
 constexpr double kScale = 1 / static_cast<double>(4294967295u - 1);  // rand_util.h:110-112
 
@@ -1447,28 +1443,6 @@ __device__ __forceinline__ void leaf_step(const SceneView& S, Stack<SE>& st, con
                     if (wave_leader()) ctr.it_leaf += 2;
                 }
                 cand = sphere_pair_candidates(cand, pair_at((LdsPair*)static_cast<uintptr_t>(S.spair_lds + ((range.x + i) << 5))), L);
-            }
-        } else if (CRT_LEAF_UNROLL) {
-            // HBM records: two a round (records i and i + 2, both in the leaf), their loads in
-            // flight together, one wait; then the last record of an odd record count. One loop
-            // waited a memory latency per record (config 4's pass 1)
-            uint32_t i = 0;
-            for (; i + 2 < range.y; i += 4) {
-                const DevSpherePair r0 = pair_at((GlobalPair*)(S.spair + range.x + i));
-                const DevSpherePair r1 = pair_at((GlobalPair*)(S.spair + range.x + i + 2));
-                if (COUNT) {
-                    ctr.sphere_tests += i + 3 < range.y ? 4 : 3;
-                    if (wave_leader()) ctr.it_leaf += 4;
-                }
-                cand = sphere_pair_candidates(cand, r0, L);
-                cand = sphere_pair_candidates(cand, r1, L);
-            }
-            if (i < range.y) {
-                if (COUNT) {
-                    ctr.sphere_tests += i + 1 < range.y ? 2 : 1;
-                    if (wave_leader()) ctr.it_leaf += 2;
-                }
-                cand = sphere_pair_candidates(cand, pair_at((GlobalPair*)(S.spair + range.x + i)), L);
             }
         } else {
             for (uint32_t i = 0; i < range.y; i += 2) {
@@ -3284,7 +3258,7 @@ const char* device_build_info() {
     return "arch=" CRT_ARCH " CRT_BLOCK=" CRT_STR(CRT_BLOCK) " CRT_TILE_W=" CRT_STR(CRT_TILE_W)
            " CRT_WAVES_PER_EU=" CRT_STR(CRT_WAVES_PER_EU) " CRT_WAVES_PER_EU_LDS=" CRT_STR(CRT_WAVES_PER_EU_LDS)
            " CRT_SHADE_BATCH=" CRT_STR(CRT_SHADE_BATCH) " CRT_CHUNK_MIN=" CRT_STR(CRT_CHUNK_MIN)
-           " CRT_WATCHDOG=" CRT_STR(CRT_WATCHDOG) " CRT_PAIR_WALK=" CRT_STR(CRT_PAIR_WALK) " CRT_LEAF_UNROLL=" CRT_STR(CRT_LEAF_UNROLL);
+           " CRT_WATCHDOG=" CRT_STR(CRT_WATCHDOG) " CRT_PAIR_WALK=" CRT_STR(CRT_PAIR_WALK);
 }
 
 }  // namespace crt
