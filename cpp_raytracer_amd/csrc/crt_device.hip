@@ -1263,9 +1263,6 @@ __device__ __forceinline__ uint32_t vsel(uint64_t m, uint32_t a, uint32_t b) {
 // The step's two f32 nodes: f (the first) and g = f ^ 32, read from the LDS treelet or from HBM
 // (the treelet holds whole sibling pairs, dispatch_render, so f and g are on the same side),
 // both sides in flight together as in fetch_nodef.
-// The step's two f32 nodes: f (the first) and g = f ^ 32, read from the LDS treelet or from HBM
-// (the treelet holds whole sibling pairs, dispatch_render, so f and g are on the same side),
-// both sides in flight together as in fetch_nodef.
 template <bool TOP>
 __device__ __forceinline__ void fetch_two(const SceneView& S, uint32_t f, uint32_t g, Uvec4& a0, Uvec4& a1, Uvec4& b0,
                                           Uvec4& b1) {
@@ -1314,11 +1311,6 @@ __device__ __forceinline__ void node_lohi(const Uvec4& q0, const Uvec4& q1, cons
     lo = vmax3(vmin(x0, x1), vmin(y0, y1), vmax_s(vmin(z0, z1), tmin32));
     hi = vmin3(vmax(x0, x1), vmax(y0, y1), vmin(vmax(z0, z1), R.tmax32));
 }
-__device__ __forceinline__ float vmax3_abs(float a, float b, float c) {
-    float r;
-    asm("v_max3_f32 %0, |%1|, |%2|, |%3|" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-    return r;
-}
 
 template <typename SE, bool COUNT, bool TOP, bool INVL>
 __device__ __forceinline__ void walk_pairs(const SceneView& S, Stack<SE>& st, const double o[3], const double d[3],
@@ -1346,11 +1338,13 @@ __device__ __forceinline__ void walk_pairs(const SceneView& S, Stack<SE>& st, co
             node_lohi(a0, a1, R, tmin32, lo1, hi1);
             node_lohi(b0, b1, R, tmin32, lo2, hi2);
             const float g1 = hi1 - lo1, g2 = hi2 - lo2;
-            // one threshold for both nodes: walk()'s bound holds for any M at least each node's
-            // own max(|lo'|, |hi'|) (v_max ignores a NaN operand; a node tested alone has a sibling
-            // of finite bounds, except the sentinel's, past the node array: at worst its step is
-            // decided in f64)
-            const float t1 = __builtin_fmaf(vmax_abs(vmax3_abs(lo1, hi1, lo2), hi2), 0x1p-19f, R.marg), t2 = t1;
+            // each node its own threshold (walk()'s bound, M = max(|lo'|, |hi'|) of that node).
+            // One shared threshold (the larger M) would save a VALU a step but leaves 16x as many
+            // node tests to f64: a sibling missed on an axis the ray runs almost parallel to has
+            // |lo'| ~ |inv|, and its M made the other node's gap undecidable (config 4: 1.49e9
+            // f64 node tests a frame, 13% of walk iterations with one)
+            const float t1 = __builtin_fmaf(vmax_abs(lo1, hi1), 0x1p-19f, R.marg);
+            const float t2 = __builtin_fmaf(vmax_abs(lo2, hi2), 0x1p-19f, R.marg);
             const uint64_t two = __ballot(cur == f);  // the sibling is tested too
             uint64_t e1 = __ballot(g1 > 0.f), e2 = __ballot(g2 > 0.f) & two;
             const uint64_t u1 = __ballot(!(fabsf(g1) > t1)), u2 = two & __ballot(!(fabsf(g2) > t2));
