@@ -331,9 +331,46 @@ def test_pair_walk_equals_node_walk(crt, monkeypatch, name, seed, kw):
     s = crt.GpuScene(d, build_device=0 if name == "millions" else None)
     cam = crt.resolve_camera(d.camera, 41)
     pair, _ = s.render(cam, 1)
+    pair_f64 = f64_node_tests(s, cam, monkeypatch)
     monkeypatch.setenv("CRT_NO_PAIR_WALK", "1")
     node, _ = s.render(cam, 1)
+    node_f64 = f64_node_tests(s, cam, monkeypatch)
     assert pair.tobytes() == node.tobytes()
     assert s.guard(0) == 0
+    # the pair walk leaves no more node tests to f64 than the one-node walk (a threshold shared by
+    # a pair's two nodes once left 16x as many, round 6)
+    assert pair_f64 <= 1.1 * node_f64 + 64, (pair_f64, node_f64)
     if name != "millions":  # the oracle's millions build alone takes ~10 s
         check(pair, orc.render(d, 41, threads=8))
+
+
+def f64_node_tests(s, cam, monkeypatch):
+    """Node tests the instrumented pass decided in f64, walking like the timed kernel."""
+    s.upload(0)
+    with monkeypatch.context() as m:
+        m.setenv("CRT_COUNT_SPEC", "1")
+        return s.render_count(0, cam).slow_node_tests
+
+
+@pytest.mark.parametrize("name,seed,view", [
+    ("rtow_final", 42, dict(center=(0.0, 1.0, 14.0), lookat=(0.0, 1.0, 0.0))),
+    ("christmas_tree", None, dict(center=(0.0, 10.0, 50.0), direction=(0.0, 0.0, -1.0))),
+])
+def test_pair_walk_axis_aligned_camera(crt, monkeypatch, name, seed, view):
+    """Primary rays almost parallel to the z axis (camera on the axis, no defocus): their slab
+    values on x and y are huge for boxes the ray misses there, which is what a threshold shared
+    by both nodes of a pair step turned into undecidable f32 tests (round 6). The pair walk with
+    per-node thresholds still gives the one-node walk's frame bit for bit, and the oracle's."""
+    monkeypatch.setenv("CRT_NO_LDS_SCENE", "1")
+    d = scene(crt, name, seed, image_w=64, image_h=48, samples_per_pixel=4, max_depth=20, defocus_angle=0.0,
+              **view)
+    s = crt.GpuScene(d)
+    cam = crt.resolve_camera(d.camera, 43)
+    pair, _ = s.render(cam, 1)
+    pair_f64 = f64_node_tests(s, cam, monkeypatch)
+    monkeypatch.setenv("CRT_NO_PAIR_WALK", "1")
+    node, _ = s.render(cam, 1)
+    node_f64 = f64_node_tests(s, cam, monkeypatch)
+    assert pair.tobytes() == node.tobytes()
+    assert pair_f64 <= 1.1 * node_f64 + 64, (pair_f64, node_f64)
+    check(pair, orc.render(d, 43, threads=8))
