@@ -344,6 +344,24 @@ def test_pair_walk_equals_node_walk(crt, monkeypatch, name, seed, kw):
         check(pair, orc.render(d, 41, threads=8))
 
 
+@pytest.mark.parametrize("name,seed,kw,limit", [
+    ("rtow_final", 42, dict(image_w=120, image_h=80, samples_per_pixel=8, max_depth=50), 1e-3),
+    ("millions", 42, dict(image_w=96, image_h=54, samples_per_pixel=4, max_depth=50), 1e-2),
+])
+def test_f32_walk_decides_almost_every_node(crt, monkeypatch, name, seed, kw, limit):
+    """The f32 node test leaves few decisions to f64 (config 2: 8.6e-5 of node tests, config 4
+    with the pair walk 1.9e-3). A change that keeps frames bit-identical but makes many gaps
+    undecidable (round 6's med3 form of the slab clamp: 0.5% on config 2, 6-8% slower) fails here."""
+    d = scene(crt, name, seed, **kw)
+    s = crt.GpuScene(d, build_device=0 if name == "millions" else None)
+    cam = crt.resolve_camera(d.camera, 44)
+    s.upload(0)
+    monkeypatch.setenv("CRT_COUNT_SPEC", "1")
+    st = s.render_count(0, cam)
+    assert st.nodes_visited > 0
+    assert st.slow_node_tests <= limit * st.nodes_visited, (st.slow_node_tests, st.nodes_visited)
+
+
 def f64_node_tests(s, cam, monkeypatch):
     """Node tests the instrumented pass decided in f64, walking like the timed kernel."""
     s.upload(0)
